@@ -1,0 +1,84 @@
+/*
+ * lzo_mi355x.h -- batch C-ABI of the MI355X LZO1X codec (liblzo_mi355x.so).
+ *
+ * The reference has no batch interface: every caller invokes the single-block
+ * functions of lib/minilzo.h synchronously.  These entry
+ * points let the same callers hand over many ITB-sized blocks at once:
+ *   - mds/txg.c:700-770   (txg_wb_itb: one lzo1x_1_compress per dirty ITB)
+ *   - mds/itb.c:2949-2980, mdsl/gc.c:755-786 (itb_lzo_decompress per ITB)
+ *   - api/api.c:6509-6541, :6427-6446 (client column data)
+ * Output of every block is identical to the single-block functions in
+ * minilzo.h (and so to lib/minilzo.c with a zero-filled wrkmem).
+ *
+ * Plain C types only: pointers, sizes, and the HIP stream as void*.
+ */
+#ifndef POM_LZO_MI355X_H
+#define POM_LZO_MI355X_H 1
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Worst-case LZO1X-1 output for n input bytes: n + n/16 + 64 + 3. */
+size_t lzo_mi355x_worst_compress(size_t n);
+
+/* Number of usable GPUs (0 when none: every codec call then fails). */
+int lzo_mi355x_device_count(void);
+
+/* ---- device-resident batches ------------------------------------------------
+ * All pointers are device (HBM) pointers; the call only enqueues work on
+ * `stream` (a hipStream_t, NULL = default stream) and returns 0 or -1 on a
+ * launch failure.  Block b reads src + src_off[b] .. + src_len[b] and writes
+ * at most dst_cap[b] bytes at dst + dst_off[b]; out_len[b] and status[b]
+ * (LZO_E_* code) are written when the stream reaches the work.
+ */
+int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
+                            const uint32_t *src_len, uint8_t *dst,
+                            const uint64_t *dst_off, const uint32_t *dst_cap,
+                            uint32_t *out_len, int32_t *status, uint32_t nblocks,
+                            void *stream);
+
+/* Decompression with lzo1x_decompress_safe semantics per block (capacity
+ * dst_cap[b]).  `scratch` is device memory of lzo_mi355x_decompress_scratch()
+ * bytes for nblocks (may be NULL when that is 0). */
+int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
+                              const uint32_t *src_len, uint8_t *dst,
+                              const uint64_t *dst_off, const uint32_t *dst_cap,
+                              uint32_t *out_len, int32_t *status, uint32_t nblocks,
+                              void *scratch, void *stream);
+size_t lzo_mi355x_decompress_scratch(uint32_t nblocks);
+
+/* Decoded length of each block (the unchecked decoder's view), no output. */
+int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,
+                                  const uint32_t *src_len, uint32_t *out_len,
+                                  int32_t *status, uint32_t nblocks, void *stream);
+
+/* Decoded length of one host-resident LZO1X stream (GPU pre-scan): the size
+ * the destination of lzo1x_decompress() must have.  Returns the status the
+ * decoder would return with unlimited capacity; *dst_len = bytes it produces. */
+int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len,
+                              unsigned long *dst_len);
+
+/* ---- host-resident batches --------------------------------------------------
+ * Blocks start and end in host memory (the mdsl/aio.c write path and the
+ * xnet wire).  Blocks are packed into pinned staging, copied to the GPU with
+ * hipMemcpyAsync, coded, and copied back.  Synchronous; thread-safe (each
+ * host thread owns its stream and staging).  Returns 0, or LZO_E_ERROR when
+ * the GPU is unusable; per-block results are in status[].
+ */
+int lzo_mi355x_compress_batch(const uint8_t *const *src, const size_t *src_len,
+                              uint8_t *const *dst, size_t *dst_len, int *status,
+                              size_t nblocks);
+/* dst_len[b] is the capacity in and the produced length out. */
+int lzo_mi355x_decompress_batch(const uint8_t *const *src, const size_t *src_len,
+                                uint8_t *const *dst, size_t *dst_len, int *status,
+                                size_t nblocks);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* POM_LZO_MI355X_H */

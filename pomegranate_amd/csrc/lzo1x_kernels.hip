@@ -1,0 +1,717 @@
+// lzo1x_kernels.hip -- LZO1X-1 encode / LZO1X decode kernels for MI355X
+// (gfx950, CDNA4), written for 64-lane wavefronts.  One block per workgroup of
+// one wave; everything the wave decides is wave-uniform and lives in SGPRs,
+// the byte moving is spread over the 64 lanes.
+//
+// Reference behaviour (paths relative to the reference tree):
+//   encoder  lib/minilzo.c:2922-3207  (lzo1x_1_compress, zero-filled wrkmem)
+//   decoder  lib/minilzo.c:3308-3699  (lzo1x_decompress) with the checks of
+//            lib/minilzo.c:3703-4190   (lzo1x_decompress_safe)
+// The behavioral spec these kernels implement is SURVEY.md Appendix A.
+//
+// Device-side batch layout (SoA, all in HBM):
+//   src + src_off[b] .. + src_len[b]   input block b
+//   dst + dst_off[b] .. + dst_cap[b]   output region of block b
+//   out_len[b], status[b]              results (LZO_E_* codes)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lzo_mi355x_kernels.h"
+
+namespace {
+
+constexpr int kWave = 64;
+
+constexpr int E_OK = 0;
+constexpr int E_ERROR = -1;
+constexpr int E_INPUT_OVERRUN = -4;
+constexpr int E_OUTPUT_OVERRUN = -5;
+constexpr int E_LOOKBEHIND_OVERRUN = -6;
+constexpr int E_EOF_NOT_FOUND = -7;
+constexpr int E_INPUT_NOT_CONSUMED = -8;
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint32_t ctz64(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+// Compiler-only ordering point between LDS passes of one wave: the LDS unit
+// executes one wave's DS instructions in issue order, so read-after-write
+// across lanes needs no wait, only that the compiler keeps program order.
+__device__ __forceinline__ void wave_order() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+
+// ---------------------------------------------------------------------------
+// Input window: 256 bytes of the compressed block held one dword per lane.
+// Wave-uniform reads extract a byte with v_readlane (no memory round trip);
+// bytes at or past len read as 0 (oracle convention, see lzo1x_oracle.c).
+// ---------------------------------------------------------------------------
+struct InWin {
+    const uint8_t* in;
+    uint32_t len;
+    int64_t r0;   // block-relative index of the first byte of lane 0's dword
+    uint32_t w;   // this lane's dword
+};
+
+__device__ __forceinline__ void win_load(InWin& W, uint32_t at)
+{
+    const uintptr_t base = (uintptr_t)W.in;
+    const uint32_t hist = at > 32 ? 32u : at;
+    const uintptr_t a0 = (base + at - hist) & ~(uintptr_t)3;
+    W.r0 = (int64_t)(a0 - base);
+    const int64_t r = W.r0 + 4 * (int64_t)lane_id();
+    uint32_t v = 0;
+    if (r + 4 > 0 && r < (int64_t)W.len) {
+        // an aligned dword overlapping [0, len) never leaves the allocation's page
+        v = *(const uint32_t*)(a0 + 4 * (uintptr_t)lane_id());
+        if (r < 0)
+            v &= ~0u << (uint32_t)(8 * -r);
+        if (r + 4 > (int64_t)W.len)
+            v &= ~0u >> (uint32_t)(8 * (r + 4 - (int64_t)W.len));
+    }
+    W.w = v;
+}
+
+__device__ __forceinline__ uint32_t win_byte(InWin& W, uint32_t i)
+{
+    if (i >= W.len)
+        return 0;
+    int64_t rel = (int64_t)i - W.r0;
+    if (rel < 0 || rel >= 4 * kWave) {
+        win_load(W, i);
+        rel = (int64_t)i - W.r0;
+    }
+    const uint32_t d = lane_read(W.w, (uint32_t)(rel >> 2));
+    return (d >> (8u * ((uint32_t)rel & 3u))) & 0xFFu;
+}
+
+// ---------------------------------------------------------------------------
+// Exact decoder.  Mirrors the grammar walk of lib/minilzo.c:3308-3699 under
+// the safe decoder's checks (:3703-3761); WRITE=false is the length pre-scan
+// used by the unchecked single-call API (capacity unknown to the callee).
+// Output goes through a 64 KiB LDS ring (LZO1X looks back at most 0xBFFF
+// bytes, lib/minilzo.c:2653) and is flushed to HBM in 8 KiB pieces.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRing = 65536;
+constexpr uint32_t kRingMask = kRing - 1;
+constexpr uint32_t kFlushQ = 8192;
+
+template <bool WRITE>
+struct Dec {
+    InWin W;
+    uint8_t* ring;
+    uint8_t* out;
+    uint32_t cap;
+    uint32_t ip, op, flushed;
+};
+
+template <bool WRITE>
+__device__ __forceinline__ void dec_flush(Dec<WRITE>& d, uint32_t upto)
+{
+    if (!WRITE)
+        return;
+    wave_order();
+    const uint32_t l = lane_id();
+    for (uint32_t k = d.flushed; k < upto; k += kWave) {
+        const uint32_t j = k + l;
+        if (j < upto)
+            d.out[j] = d.ring[j & kRingMask];
+    }
+    d.flushed = upto;
+    wave_order();
+}
+
+template <bool WRITE>
+__device__ __forceinline__ void dec_maybe_flush(Dec<WRITE>& d)
+{
+    if (WRITE && d.op - d.flushed >= kFlushQ)
+        dec_flush(d, d.op);
+}
+
+template <bool WRITE>
+__device__ __forceinline__ void dec_lits(Dec<WRITE>& d, uint32_t t)
+{
+    if (WRITE) {
+        const uint32_t l = lane_id();
+        while (t > 0) {
+            const uint32_t c = t < (uint32_t)kWave ? t : (uint32_t)kWave;
+            if (l < c) {
+                const uint32_t si = d.ip + l;
+                d.ring[(d.op + l) & kRingMask] = si < d.W.len ? d.W.in[si] : (uint8_t)0;
+            }
+            wave_order();
+            d.ip += c;
+            d.op += c;
+            t -= c;
+            dec_maybe_flush(d);
+        }
+    } else {
+        d.ip += t;
+        d.op += t;
+    }
+}
+
+// Forward copy of len bytes from dist back; overlapping copies repeat with
+// period dist (byte-serial semantics of lib/minilzo.c:3622-3646).
+template <bool WRITE>
+__device__ __forceinline__ void dec_back(Dec<WRITE>& d, uint32_t dist, uint32_t len)
+{
+    if (!WRITE) {
+        d.op += len;
+        return;
+    }
+    const uint32_t l = lane_id();
+    const uint32_t step = dist >= (uint32_t)kWave ? (uint32_t)kWave : dist * ((uint32_t)kWave / dist);
+    const uint32_t period = dist >= (uint32_t)kWave ? dist : step;
+    bool first = true;
+    while (len > 0) {
+        const uint32_t c = len < step ? len : step;
+        if (l < c) {
+            const uint32_t src = first ? d.op - dist + (dist >= (uint32_t)kWave ? l : l % dist)
+                                       : d.op + l - period;
+            const uint8_t v = d.ring[src & kRingMask];
+            d.ring[(d.op + l) & kRingMask] = v;
+        }
+        wave_order();
+        first = false;
+        d.op += c;
+        len -= c;
+        dec_maybe_flush(d);
+    }
+}
+
+template <bool WRITE>
+__device__ __forceinline__ bool dec_need_ip(const Dec<WRITE>& d, uint32_t x)
+{
+    // lib/minilzo.c:3733-3734: (lzo_uint)(ip_end - ip) < x; passes once ip > ip_end
+    return !(d.ip <= d.W.len && d.W.len - d.ip < x);
+}
+
+template <bool WRITE>
+__device__ __forceinline__ bool dec_need_op(const Dec<WRITE>& d, uint32_t x)
+{
+    return d.cap - d.op >= x;
+}
+
+template <bool WRITE>
+__device__ __forceinline__ bool dec_ext(Dec<WRITE>& d, uint32_t base, uint32_t& t)
+{
+    if (!dec_need_ip(d, 1))
+        return false;
+    uint32_t v = 0;
+    while (win_byte(d.W, d.ip) == 0) {
+        v += 255;
+        d.ip++;
+        if (!dec_need_ip(d, 1))
+            return false;
+    }
+    t = v + base + win_byte(d.W, d.ip);
+    d.ip++;
+    return true;
+}
+
+template <bool WRITE>
+__device__ int dec_run(Dec<WRITE>& d)
+{
+    uint32_t t, dist, len;
+    int where;
+    t = win_byte(d.W, 0);
+    if (t > 17) {                                   // lib/minilzo.c:3357-3365
+        d.ip = 1;
+        t -= 17;
+        if (t < 4)
+            where = 3;
+        else {
+            if (!dec_need_op(d, t)) return E_OUTPUT_OVERRUN;
+            if (!dec_need_ip(d, t + 1)) return E_INPUT_OVERRUN;
+            dec_lits(d, t);
+            where = 1;
+        }
+    } else
+        where = 0;
+
+    for (;;) {
+        if (where == 0) {                           // :3367-3414
+            if (!(d.ip < d.W.len))
+                return E_EOF_NOT_FOUND;
+            t = win_byte(d.W, d.ip++);
+            if (t >= 16) {
+                where = 2;
+                continue;
+            }
+            if (t == 0 && !dec_ext(d, 15, t))
+                return E_INPUT_OVERRUN;
+            if (!dec_need_op(d, t + 3)) return E_OUTPUT_OVERRUN;
+            if (!dec_need_ip(d, t + 4)) return E_INPUT_OVERRUN;
+            dec_lits(d, t + 3);
+            where = 1;
+            continue;
+        }
+        if (where == 1) {                           // :3416-3443
+            t = win_byte(d.W, d.ip++);
+            if (t >= 16) {
+                where = 2;
+                continue;
+            }
+            dist = 1 + 0x800 + (t >> 2) + (win_byte(d.W, d.ip++) << 2);
+            if (dist > d.op) return E_LOOKBEHIND_OVERRUN;
+            if (!dec_need_op(d, 3)) return E_OUTPUT_OVERRUN;
+            dec_back(d, dist, 3);
+        } else if (where == 2) {                    // :3446-3646
+            if (t >= 64) {
+                dist = 1 + ((t >> 2) & 7) + (win_byte(d.W, d.ip++) << 3);
+                len = (t >> 5) + 1;
+            } else if (t >= 32) {
+                len = t & 31;
+                if (len == 0 && !dec_ext(d, 31, len))
+                    return E_INPUT_OVERRUN;
+                len += 2;
+                const uint32_t lo = win_byte(d.W, d.ip);
+                const uint32_t hi = win_byte(d.W, d.ip + 1);
+                dist = 1 + ((lo | (hi << 8)) >> 2);
+                d.ip += 2;
+            } else if (t >= 16) {
+                uint32_t dd = (t & 8) << 11;
+                len = t & 7;
+                if (len == 0 && !dec_ext(d, 7, len))
+                    return E_INPUT_OVERRUN;
+                len += 2;
+                const uint32_t lo = win_byte(d.W, d.ip);
+                const uint32_t hi = win_byte(d.W, d.ip + 1);
+                dd += (lo | (hi << 8)) >> 2;
+                d.ip += 2;
+                if (dd == 0) {                      // EOF marker, :3580-3581, 3676-3680
+                    if (d.ip == d.W.len) return E_OK;
+                    return d.ip < d.W.len ? E_INPUT_NOT_CONSUMED : E_INPUT_OVERRUN;
+                }
+                dist = dd + 0x4000;
+            } else {
+                dist = 1 + (t >> 2) + (win_byte(d.W, d.ip++) << 2);
+                len = 2;
+            }
+            if (dist > d.op) return E_LOOKBEHIND_OVERRUN;
+            if (!dec_need_op(d, len)) return E_OUTPUT_OVERRUN;
+            dec_back(d, dist, len);
+        }
+        if (where != 3) {                           // match_done, :3650-3653
+            t = win_byte(d.W, d.ip - 2) & 3;
+            if (t == 0) {
+                where = 0;
+                continue;
+            }
+        }
+        // match_next, :3654-3668
+        if (!dec_need_op(d, t)) return E_OUTPUT_OVERRUN;
+        if (!dec_need_ip(d, t + 1)) return E_INPUT_OVERRUN;
+        dec_lits(d, t);
+        t = win_byte(d.W, d.ip++);
+        if (!(d.ip < d.W.len))
+            return E_EOF_NOT_FOUND;
+        where = 2;
+    }
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+    const uint32_t* __restrict__ only, uint32_t nblocks)
+{
+    __shared__ uint8_t ring[WRITE ? kRing : 4];
+    const uint32_t b = only ? only[blockIdx.x] : blockIdx.x;
+    if (b >= nblocks)
+        return;
+    Dec<WRITE> d;
+    d.W.in = src + src_off[b];
+    d.W.len = src_len[b];
+    d.W.r0 = -((int64_t)1 << 40);     // empty window: the first read loads it
+    d.W.w = 0;
+    d.ring = ring;
+    d.out = dst ? dst + dst_off[b] : nullptr;
+    d.cap = dst_cap ? dst_cap[b] : 0xFFFFFFFFu;
+    d.ip = d.op = d.flushed = 0;
+    const int rc = dec_run(d);
+    dec_flush(d, d.op);
+    if (lane_id() == 0) {
+        out_len[b] = d.op;
+        status[b] = rc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Encoder: LZO1X-1 greedy parse with the dictionary
+// in LDS.  The wave probes 64 consecutive positions at once; lanes whose
+// dictionary slots could have been written by an earlier lane of the same
+// window are cut off (conflict claims in the slot word's top bits), the first
+// matching lane ends the window, and the writes of the lanes before it are
+// committed in position order with ds_max.
+//   dict word: [31:25] claiming lane (0x7F = none), [24:0] position+1 (0 = EMPTY)
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSlots = 1u << 14;            // D_BITS 14, lib/minilzo.c:2627
+constexpr uint32_t kPosMask = (1u << 25) - 1;
+constexpr uint32_t kNoClaim = 0x7Fu << 25;
+constexpr uint32_t kStage = 8192;
+constexpr uint32_t kStageMask = kStage - 1;
+constexpr uint32_t kStageFlush = 4096;
+
+struct Enc {
+    const uint8_t* in;
+    uint32_t n;
+    uint8_t* out;
+    uint32_t cap;
+    uint8_t* stage;
+    uint32_t op, flushed;
+};
+
+__device__ __forceinline__ void enc_flush(Enc& e, uint32_t upto)
+{
+    wave_order();
+    const uint32_t l = lane_id();
+    for (uint32_t k = e.flushed; k < upto; k += kWave) {
+        const uint32_t j = k + l;
+        if (j < upto && j < e.cap)
+            e.out[j] = e.stage[j & kStageMask];
+    }
+    e.flushed = upto;
+    wave_order();
+}
+
+// Keep the last two bytes staged: a following short literal run ORs its
+// length into out[op-2] (lib/minilzo.c:3027-3030, 3181-3182).
+__device__ __forceinline__ void enc_maybe_flush(Enc& e)
+{
+    if (e.op - e.flushed >= kStageFlush + 2)
+        enc_flush(e, e.op - 2);
+}
+
+__device__ __forceinline__ void enc_byte(Enc& e, uint32_t v)
+{
+    if (lane_id() == 0)
+        e.stage[e.op & kStageMask] = (uint8_t)v;
+    wave_order();
+    e.op++;
+}
+
+__device__ __forceinline__ void enc_patch(Enc& e, uint32_t v)
+{
+    if (lane_id() == 0)
+        e.stage[(e.op - 2) & kStageMask] |= (uint8_t)v;
+    wave_order();
+}
+
+__device__ __forceinline__ void enc_zeros(Enc& e, uint32_t count)
+{
+    const uint32_t l = lane_id();
+    while (count > 0) {
+        const uint32_t c = count < (uint32_t)kWave ? count : (uint32_t)kWave;
+        if (l < c)
+            e.stage[(e.op + l) & kStageMask] = 0;
+        wave_order();
+        e.op += c;
+        count -= c;
+        enc_maybe_flush(e);
+    }
+}
+
+// ext(x): x/255 zero bytes then the remainder (lib/minilzo.c:3034-3046)
+__device__ __forceinline__ void enc_ext(Enc& e, uint32_t x)
+{
+    const uint32_t z = (x - 1) / 255;
+    enc_zeros(e, z);
+    enc_byte(e, x - 255 * z);
+}
+
+__device__ __forceinline__ void enc_lits(Enc& e, uint32_t from, uint32_t count)
+{
+    const uint32_t l = lane_id();
+    while (count > 0) {
+        const uint32_t c = count < (uint32_t)kWave ? count : (uint32_t)kWave;
+        if (l < c)
+            e.stage[(e.op + l) & kStageMask] = e.in[from + l];
+        wave_order();
+        e.op += c;
+        from += c;
+        count -= c;
+        enc_maybe_flush(e);
+    }
+}
+
+// Literal-run header (lib/minilzo.c:3023-3048, tail :3179-3199)
+__device__ __forceinline__ void enc_lit_header(Enc& e, uint32_t r)
+{
+    if (r <= 3)
+        enc_patch(e, r);
+    else if (r <= 18)
+        enc_byte(e, r - 3);
+    else {
+        enc_byte(e, 0);
+        enc_ext(e, r - 18);
+    }
+}
+
+// Match token (lib/minilzo.c:3064-3145)
+__device__ __forceinline__ void enc_match(Enc& e, uint32_t len, uint32_t off)
+{
+    if (len <= 8) {
+        if (off <= 0x800) {
+            const uint32_t o = off - 1;
+            enc_byte(e, ((len - 1) << 5) | ((o & 7) << 2));
+            enc_byte(e, o >> 3);
+            return;
+        }
+        if (off <= 0x4000) {
+            const uint32_t o = off - 1;
+            enc_byte(e, 0x20 | (len - 2));
+            enc_byte(e, (o & 63) << 2);
+            enc_byte(e, o >> 6);
+            return;
+        }
+        const uint32_t o = off - 0x4000;
+        enc_byte(e, 0x10 | ((o & 0x4000) >> 11) | (len - 2));
+        enc_byte(e, (o & 63) << 2);
+        enc_byte(e, o >> 6);
+        return;
+    }
+    uint32_t o;
+    if (off <= 0x4000) {
+        o = off - 1;
+        if (len <= 33)
+            enc_byte(e, 0x20 | (len - 2));
+        else {
+            enc_byte(e, 0x20);
+            enc_ext(e, len - 33);
+        }
+    } else {
+        o = off - 0x4000;
+        const uint32_t hi = (o & 0x4000) >> 11;
+        if (len <= 9)
+            enc_byte(e, 0x10 | hi | (len - 2));
+        else {
+            enc_byte(e, 0x10 | hi);
+            enc_ext(e, len - 9);
+        }
+    }
+    enc_byte(e, (o & 63) << 2);
+    enc_byte(e, o >> 6);
+}
+
+__device__ __forceinline__ uint32_t slot_primary(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3)
+{
+    uint32_t v = (((b3 << 6) ^ b2) << 5) ^ b1;     // DX3(p,5,5,6), lib/minilzo.c:2697-2704
+    v = (v << 5) ^ b0;
+    return ((v * 33u) >> 5) & (kSlots - 1);       // D_INDEX1, :2629
+}
+
+__device__ __forceinline__ uint32_t slot_secondary(uint32_t h)
+{
+    return (h & 0x7FFu) ^ 0x201Fu;                // D_INDEX2, :2630
+}
+
+// Greedy parse over in[0, n), n > 13.  Returns the tail length (n - ii).
+__device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
+{
+    const uint32_t l = lane_id();
+    const uint8_t* in = e.in;
+    const uint32_t n = e.n;
+    const uint32_t ip_end = n - 13;                // lib/minilzo.c:2929
+    uint32_t ip = 4, ii = 0;
+
+    for (;;) {
+        const uint32_t p = ip + l;
+        const bool active = l == 0 || p < ip_end;
+        uint32_t h1 = 0, h2 = 0, w1 = 0, w2 = 0, b3 = 0, b0 = 0, b1 = 0, b2 = 0;
+        if (active) {
+            b0 = in[p];
+            b1 = in[p + 1];
+            b2 = in[p + 2];
+            b3 = in[p + 3];
+            h1 = slot_primary(b0, b1, b2, b3);
+            h2 = slot_secondary(h1);
+            w1 = dict[h1];
+            w2 = dict[h2];
+        }
+        wave_order();
+        if (active) {
+            atomicMin(&dict[h1], (l << 25) | (w1 & kPosMask));
+            atomicMin(&dict[h2], (l << 25) | (w2 & kPosMask));
+        }
+        wave_order();
+        bool conflicted = false;
+        if (active) {
+            const uint32_t m1 = dict[h1] >> 25;
+            const uint32_t m2 = dict[h2] >> 25;
+            conflicted = m1 < l || m2 < l;
+        }
+        wave_order();
+        if (active) {
+            atomicOr(&dict[h1], kNoClaim);
+            atomicOr(&dict[h2], kNoClaim);
+        }
+        wave_order();
+        const uint64_t cm = wave_ballot(conflicted);
+        const uint64_t am = wave_ballot(active);
+        const uint32_t navail = cm ? ctz64(cm) : (uint32_t)__builtin_popcountll(am);
+
+        // Probe decision with the pre-window dictionary (exact for l < navail).
+        bool ok = false;
+        uint32_t slot = h1, cand = 0;
+        if (l < navail) {
+            const uint32_t c1 = (w1 & kPosMask) - 1;
+            const bool v1 = (w1 & kPosMask) != 0 && p - c1 <= 0xBFFFu;
+            const uint32_t c2 = (w2 & kPosMask) - 1;
+            const bool v2 = (w2 & kPosMask) != 0 && p - c2 <= 0xBFFFu;
+            if (v1) {
+                if (p - c1 <= 0x800u || in[c1 + 3] == b3) {
+                    ok = true;
+                    cand = c1;
+                } else {
+                    slot = h2;
+                    if (v2 && (p - c2 <= 0x800u || in[c2 + 3] == b3)) {
+                        ok = true;
+                        cand = c2;
+                    }
+                }
+            }
+            if (ok)        // try_match, lib/minilzo.c:2962-2971
+                ok = in[cand] == b0 && in[cand + 1] == b1 && in[cand + 2] == b2;
+        }
+        const uint64_t mm = wave_ballot(ok);
+        const uint32_t ndone = mm ? ctz64(mm) + 1 : navail;
+        if (l < ndone)     // UPDATE_I in position order
+            atomicMax(&dict[slot], kNoClaim | (p + 1));
+        wave_order();
+
+        if (!mm) {
+            ip += ndone;
+            if (ip >= ip_end)
+                break;
+            continue;
+        }
+        const uint32_t q = ndone - 1;
+        const uint32_t mp = ip + q;
+        const uint32_t mc = lane_read(cand, q);
+
+        if (mp > ii) {                             // pending literals
+            enc_lit_header(e, mp - ii);
+            enc_lits(e, ii, mp - ii);
+        }
+        // Match length: first mismatch at index >= 3, capped at the block end
+        // (lib/minilzo.c:3051-3102).
+        uint32_t len;
+        for (uint32_t k = 3;; k += kWave) {
+            const uint32_t idx = k + l;
+            const bool eq = mp + idx < n && in[mc + idx] == in[mp + idx];
+            const uint64_t miss = wave_ballot(!eq);
+            if (miss) {
+                len = k + ctz64(miss);
+                break;
+            }
+        }
+        enc_match(e, len, mp - mc);
+        enc_maybe_flush(e);
+        ip = mp + len;
+        ii = ip;
+        if (ip >= ip_end)
+            break;
+    }
+    return n - ii;
+}
+
+__global__ __launch_bounds__(kWave) void lzo1x_encode_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks)
+{
+    __shared__ uint32_t dict[kSlots];
+    __shared__ uint8_t stage[kStage];
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t l = lane_id();
+    Enc e;
+    e.in = src + src_off[b];
+    e.n = src_len[b];
+    e.out = dst + dst_off[b];
+    e.cap = dst_cap[b];
+    e.stage = stage;
+    e.op = e.flushed = 0;
+    if (e.n > kPosMask - 1) {                      // positions must fit 25 bits
+        if (l == 0) {
+            out_len[b] = 0;
+            status[b] = E_ERROR;
+        }
+        return;
+    }
+
+    uint32_t t;
+    if (e.n <= 13) {                               // lib/minilzo.c:3167-3168
+        t = e.n;
+    } else {
+        for (uint32_t s = l; s < kSlots; s += kWave)
+            dict[s] = kNoClaim;                    // zero-filled wrkmem: all EMPTY
+        wave_order();
+        t = enc_parse(e, dict);
+    }
+    if (t > 0) {                                   // tail, lib/minilzo.c:3175-3199
+        const uint32_t ii = e.n - t;
+        if (e.op == 0 && t <= 238)
+            enc_byte(e, 17 + t);
+        else
+            enc_lit_header(e, t);
+        enc_lits(e, ii, t);
+    }
+    enc_byte(e, 0x11);                             // EOF, lib/minilzo.c:3201-3203
+    enc_byte(e, 0);
+    enc_byte(e, 0);
+    enc_flush(e, e.op);
+    if (l == 0) {
+        out_len[b] = e.op;
+        status[b] = e.op <= e.cap ? E_OK : E_OUTPUT_OVERRUN;
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI launchers (declared in lzo_mi355x_kernels.h).
+// ---------------------------------------------------------------------------
+extern "C" int lzo_mi355x_launch_compress(const uint8_t* src, const uint64_t* src_off,
+                                          const uint32_t* src_len, uint8_t* dst,
+                                          const uint64_t* dst_off, const uint32_t* dst_cap,
+                                          uint32_t* out_len, int32_t* status,
+                                          uint32_t nblocks, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_encode_kernel, dim3(nblocks), dim3(kWave), 0, stream, src, src_off,
+                       src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzo_mi355x_launch_decompress_exact(const uint8_t* src, const uint64_t* src_off,
+                                                  const uint32_t* src_len, uint8_t* dst,
+                                                  const uint64_t* dst_off, const uint32_t* dst_cap,
+                                                  uint32_t* out_len, int32_t* status,
+                                                  const uint32_t* only, uint32_t ngrid,
+                                                  uint32_t nblocks, hipStream_t stream)
+{
+    if (ngrid == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_decode_exact_kernel<true>, dim3(ngrid), dim3(kWave), 0, stream, src,
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, only, nblocks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzo_mi355x_launch_decoded_length(const uint8_t* src, const uint64_t* src_off,
+                                                const uint32_t* src_len, uint32_t* out_len,
+                                                int32_t* status, uint32_t nblocks,
+                                                hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_decode_exact_kernel<false>, dim3(nblocks), dim3(kWave), 0, stream,
+                       src, src_off, src_len, nullptr, nullptr, nullptr, out_len, status,
+                       nullptr, nblocks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

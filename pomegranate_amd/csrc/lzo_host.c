@@ -1,0 +1,454 @@
+/*
+ * lzo_host.c -- host side of liblzo_mi355x.so, in C like the reference.
+ *
+ * Implements the minilzo.h call surface (lzo_init, lzo1x_1_compress,
+ * lzo1x_decompress, lzo1x_decompress_safe; reference lib/minilzo.c) and the
+ * batch API of lzo_mi355x.h on top of the HIP kernels.  Every codec call runs
+ * on the GPU; there is no CPU codec in this library.  A call made without a
+ * usable GPU returns LZO_E_ERROR and says why on stderr once.
+ *
+ * Threading: callers are MDS commit/service threads, the MDSL
+ * GC thread and client threads.  Each host thread gets its own HIP stream and
+ * its own device/pinned staging (grown on demand, freed at thread exit), so
+ * concurrent calls never share device state.
+ */
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "lzo_mi355x.h"
+#include "lzo_mi355x_kernels.h"
+#include "minilzo.h"
+
+#define ALIGN_UP(x, a) (((x) + (size_t)(a) - 1) & ~((size_t)(a) - 1))
+
+/* ------------------------------------------------------------------------ */
+/* GPU availability (checked once per process)                              */
+/* ------------------------------------------------------------------------ */
+static pthread_once_t gpu_once = PTHREAD_ONCE_INIT;
+static int gpu_count;
+
+static void gpu_probe(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        fprintf(stderr, "liblzo_mi355x: no usable GPU (hipGetDeviceCount=%d); "
+                        "the MI355X LZO1X codec has no CPU fallback\n", n);
+        n = 0;
+    }
+    gpu_count = n;
+}
+
+int lzo_mi355x_device_count(void)
+{
+    pthread_once(&gpu_once, gpu_probe);
+    return gpu_count;
+}
+
+size_t lzo_mi355x_worst_compress(size_t n)
+{
+    return n + n / 16 + 64 + 3;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Per-thread stream and staging                                            */
+/* ------------------------------------------------------------------------ */
+struct tctx {
+    int ready;
+    int device;
+    hipStream_t stream;
+    uint8_t *dmem;
+    size_t dcap;
+    uint8_t *hmem;
+    size_t hcap;
+};
+
+static pthread_key_t tkey;
+static pthread_once_t tkey_once = PTHREAD_ONCE_INIT;
+
+static void tctx_free(void *p)
+{
+    struct tctx *t = p;
+    if (!t)
+        return;
+    if (t->ready) {
+        hipSetDevice(t->device);
+        if (t->dmem)
+            hipFree(t->dmem);
+        if (t->hmem)
+            hipHostFree(t->hmem);
+        hipStreamDestroy(t->stream);
+    }
+    free(t);
+}
+
+static void tkey_make(void)
+{
+    pthread_key_create(&tkey, tctx_free);
+}
+
+static struct tctx *tctx_get(void)
+{
+    if (lzo_mi355x_device_count() <= 0)
+        return NULL;
+    pthread_once(&tkey_once, tkey_make);
+    struct tctx *t = pthread_getspecific(tkey);
+    if (!t) {
+        t = calloc(1, sizeof(*t));
+        if (!t)
+            return NULL;
+        pthread_setspecific(tkey, t);
+    }
+    if (!t->ready) {
+        if (hipGetDevice(&t->device) != hipSuccess)
+            return NULL;
+        if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess)
+            return NULL;
+        t->ready = 1;
+    }
+    return t;
+}
+
+static int tctx_reserve(struct tctx *t, size_t dbytes, size_t hbytes)
+{
+    if (dbytes > t->dcap) {
+        if (t->dmem)
+            hipFree(t->dmem);
+        t->dmem = NULL;
+        t->dcap = 0;
+        size_t want = ALIGN_UP(dbytes + dbytes / 4, 1 << 20);
+        if (hipMalloc((void **)&t->dmem, want) != hipSuccess)
+            return -1;
+        t->dcap = want;
+    }
+    if (hbytes > t->hcap) {
+        if (t->hmem)
+            hipHostFree(t->hmem);
+        t->hmem = NULL;
+        t->hcap = 0;
+        size_t want = ALIGN_UP(hbytes + hbytes / 4, 1 << 20);
+        if (hipHostMalloc((void **)&t->hmem, want, hipHostMallocDefault) != hipSuccess)
+            return -1;
+        t->hcap = want;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Device-resident batch entry points                                       */
+/* ------------------------------------------------------------------------ */
+int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
+                            const uint32_t *src_len, uint8_t *dst,
+                            const uint64_t *dst_off, const uint32_t *dst_cap,
+                            uint32_t *out_len, int32_t *status, uint32_t nblocks,
+                            void *stream)
+{
+    return lzo_mi355x_launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
+                                      status, nblocks, (hipStream_t)stream);
+}
+
+size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
+{
+    (void)nblocks;
+    return 0;
+}
+
+int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
+                              const uint32_t *src_len, uint8_t *dst,
+                              const uint64_t *dst_off, const uint32_t *dst_cap,
+                              uint32_t *out_len, int32_t *status, uint32_t nblocks,
+                              void *scratch, void *stream)
+{
+    (void)scratch;
+    return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
+                                              out_len, status, NULL, nblocks, nblocks,
+                                              (hipStream_t)stream);
+}
+
+int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,
+                                  const uint32_t *src_len, uint32_t *out_len,
+                                  int32_t *status, uint32_t nblocks, void *stream)
+{
+    return lzo_mi355x_launch_decoded_length(src, src_off, src_len, out_len, status, nblocks,
+                                            (hipStream_t)stream);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Host-resident batches: pack -> H2D -> kernels -> D2H -> unpack           */
+/* ------------------------------------------------------------------------ */
+/* Staging layout (identical on host and device, so one copy each way):
+ *   [src_off u64][dst_off u64][src_len u32][dst_cap u32][out_len u32][status i32]
+ *   [src bytes, 16-B aligned per block][dst bytes, 16-B aligned per block] */
+struct layout {
+    size_t nb;
+    size_t o_srcoff, o_dstoff, o_srclen, o_dstcap, o_outlen, o_status;
+    size_t o_src, o_dst, total;
+    size_t src_bytes, dst_bytes;
+};
+
+static void layout_make(struct layout *L, size_t nb, const size_t *src_len, const size_t *dst_cap)
+{
+    L->nb = nb;
+    size_t o = 0;
+    L->o_srcoff = o; o += 8 * nb;
+    L->o_dstoff = o; o += 8 * nb;
+    L->o_srclen = o; o += 4 * nb;
+    L->o_dstcap = o; o += 4 * nb;
+    L->o_outlen = o; o += 4 * nb;
+    L->o_status = o; o += 4 * nb;
+    o = ALIGN_UP(o, 256);
+    L->o_src = o;
+    size_t s = 0, d = 0;
+    for (size_t b = 0; b < nb; b++) {
+        s += ALIGN_UP(src_len[b], 16);
+        d += ALIGN_UP(dst_cap[b], 16);
+    }
+    L->src_bytes = s;
+    L->dst_bytes = d;
+    o += ALIGN_UP(s, 256);
+    L->o_dst = o;
+    o += ALIGN_UP(d, 256);
+    L->total = o;
+}
+
+static void layout_fill(const struct layout *L, uint8_t *h, const uint8_t *const *src,
+                        const size_t *src_len, const size_t *dst_cap)
+{
+    uint64_t *so = (uint64_t *)(h + L->o_srcoff);
+    uint64_t *dof = (uint64_t *)(h + L->o_dstoff);
+    uint32_t *sl = (uint32_t *)(h + L->o_srclen);
+    uint32_t *dc = (uint32_t *)(h + L->o_dstcap);
+    size_t s = 0, d = 0;
+    for (size_t b = 0; b < L->nb; b++) {
+        so[b] = s;
+        dof[b] = d;
+        sl[b] = (uint32_t)src_len[b];
+        dc[b] = (uint32_t)dst_cap[b];
+        if (src_len[b])
+            memcpy(h + L->o_src + s, src[b], src_len[b]);
+        s += ALIGN_UP(src_len[b], 16);
+        d += ALIGN_UP(dst_cap[b], 16);
+    }
+}
+
+enum op_kind { OP_COMPRESS, OP_DECOMPRESS };
+
+/* Runs one staged batch.  dst_cap: capacities used by the kernels.  On
+ * return out_len/status of each block are in the pinned staging. */
+static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
+{
+    uint8_t *d = t->dmem, *h = t->hmem;
+    hipStream_t s = t->stream;
+    const uint32_t nb = (uint32_t)L->nb;
+    if (hipMemcpyAsync(d, h, L->o_dst, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -1;
+    const uint8_t *dsrc = d + L->o_src;
+    uint8_t *ddst = d + L->o_dst;
+    const uint64_t *so = (const uint64_t *)(d + L->o_srcoff);
+    const uint64_t *dof = (const uint64_t *)(d + L->o_dstoff);
+    const uint32_t *sl = (const uint32_t *)(d + L->o_srclen);
+    const uint32_t *dc = (const uint32_t *)(d + L->o_dstcap);
+    uint32_t *ol = (uint32_t *)(d + L->o_outlen);
+    int32_t *st = (int32_t *)(d + L->o_status);
+    int rc;
+    if (kind == OP_COMPRESS)
+        rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, s);
+    else
+        rc = lzo_mi355x_decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, NULL, s);
+    if (rc != 0)
+        return -1;
+    if (hipMemcpyAsync(h + L->o_outlen, d + L->o_outlen, 8 * L->nb, hipMemcpyDeviceToHost, s) !=
+        hipSuccess)
+        return -1;
+    if (L->dst_bytes &&
+        hipMemcpyAsync(h + L->o_dst, d + L->o_dst, L->dst_bytes, hipMemcpyDeviceToHost, s) !=
+            hipSuccess)
+        return -1;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
+}
+
+static int batch_common(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
+                        uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks)
+{
+    struct tctx *t = tctx_get();
+    if (!t)
+        return LZO_E_ERROR;
+    if (nblocks == 0)
+        return LZO_E_OK;
+    if (nblocks > 0xFFFFFFFFu)
+        return LZO_E_ERROR;
+    size_t *cap = malloc(nblocks * sizeof(size_t));
+    if (!cap)
+        return LZO_E_OUT_OF_MEMORY;
+    for (size_t b = 0; b < nblocks; b++) {
+        if (src_len[b] > 0xFFFFFFF0u) {
+            free(cap);
+            return LZO_E_ERROR;
+        }
+        cap[b] = kind == OP_COMPRESS ? lzo_mi355x_worst_compress(src_len[b]) : dst_len[b];
+        if (cap[b] > 0xFFFFFFF0u)
+            cap[b] = 0xFFFFFFF0u;
+    }
+    struct layout L;
+    layout_make(&L, nblocks, src_len, cap);
+    int rc = LZO_E_ERROR;
+    if (tctx_reserve(t, L.total, L.total) == 0) {
+        layout_fill(&L, t->hmem, src, src_len, cap);
+        if (run_staged(t, &L, kind) == 0) {
+            const uint32_t *ol = (const uint32_t *)(t->hmem + L.o_outlen);
+            const int32_t *st = (const int32_t *)(t->hmem + L.o_status);
+            const uint64_t *dof = (const uint64_t *)(t->hmem + L.o_dstoff);
+            for (size_t b = 0; b < nblocks; b++) {
+                size_t n = ol[b] < cap[b] ? ol[b] : cap[b];
+                if (n)
+                    memcpy(dst[b], t->hmem + L.o_dst + dof[b], n);
+                dst_len[b] = ol[b];
+                status[b] = st[b];
+            }
+            rc = LZO_E_OK;
+        }
+    }
+    free(cap);
+    return rc;
+}
+
+int lzo_mi355x_compress_batch(const uint8_t *const *src, const size_t *src_len,
+                              uint8_t *const *dst, size_t *dst_len, int *status,
+                              size_t nblocks)
+{
+    return batch_common(OP_COMPRESS, src, src_len, dst, dst_len, status, nblocks);
+}
+
+int lzo_mi355x_decompress_batch(const uint8_t *const *src, const size_t *src_len,
+                                uint8_t *const *dst, size_t *dst_len, int *status,
+                                size_t nblocks)
+{
+    return batch_common(OP_DECOMPRESS, src, src_len, dst, dst_len, status, nblocks);
+}
+
+/* ------------------------------------------------------------------------ */
+/* minilzo.h call surface                                                   */
+/* ------------------------------------------------------------------------ */
+
+/* lib/minilzo.c:2567-2598: a zero version or a type-size mismatch is
+ * LZO_E_ERROR; additionally the GPU must be usable. */
+int __lzo_init_v2(unsigned v, int s1, int s2, int s3, int s4, int s5, int s6, int s7, int s8,
+                  int s9)
+{
+    if (v == 0)
+        return LZO_E_ERROR;
+    int ok = (s1 == -1 || s1 == (int)sizeof(short)) && (s2 == -1 || s2 == (int)sizeof(int)) &&
+             (s3 == -1 || s3 == (int)sizeof(long)) &&
+             (s4 == -1 || s4 == (int)sizeof(lzo_uint32)) &&
+             (s5 == -1 || s5 == (int)sizeof(lzo_uint)) &&
+             (s6 == -1 || s6 == (int)lzo_sizeof_dict_t) &&
+             (s7 == -1 || s7 == (int)sizeof(char *)) &&
+             (s8 == -1 || s8 == (int)sizeof(lzo_voidp)) &&
+             (s9 == -1 || s9 == (int)sizeof(lzo_callback_t));
+    if (!ok)
+        return LZO_E_ERROR;
+    return lzo_mi355x_device_count() > 0 ? LZO_E_OK : LZO_E_ERROR;
+}
+
+unsigned lzo_version(void) { return LZO_VERSION; }
+const char *lzo_version_string(void) { return LZO_VERSION_STRING; }
+const char *lzo_version_date(void) { return LZO_VERSION_DATE; }
+
+int lzo1x_1_compress(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst, lzo_uintp dst_len,
+                     lzo_voidp wrkmem)
+{
+    (void)wrkmem;   /* output is the zero-filled-wrkmem output by definition */
+    const uint8_t *s[1] = { src };
+    uint8_t *d[1] = { dst };
+    size_t sl[1] = { src_len }, dl[1] = { 0 };
+    int st[1] = { LZO_E_ERROR };
+    int rc = lzo_mi355x_compress_batch(s, sl, d, dl, st, 1);
+    if (rc != LZO_E_OK)
+        return rc;
+    *dst_len = dl[0];
+    return st[0];
+}
+
+int lzo1x_decompress_safe(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst,
+                          lzo_uintp dst_len, lzo_voidp wrkmem)
+{
+    (void)wrkmem;
+    const uint8_t *s[1] = { src };
+    uint8_t *d[1] = { dst };
+    size_t sl[1] = { src_len }, dl[1] = { *dst_len };
+    int st[1] = { LZO_E_ERROR };
+    int rc = lzo_mi355x_decompress_batch(s, sl, d, dl, st, 1);
+    if (rc != LZO_E_OK)
+        return rc;
+    *dst_len = dl[0];
+    return st[0];
+}
+
+/* GPU pre-scan of one host-resident stream: decoded length and status. */
+static int prescan_one(struct tctx *t, const uint8_t *src, size_t src_len, uint32_t *olen)
+{
+    const size_t meta = 256;
+    const size_t need = meta + ALIGN_UP(src_len, 16);
+    if (tctx_reserve(t, need, need) != 0)
+        return LZO_E_ERROR;
+    uint8_t *h = t->hmem, *d = t->dmem;
+    uint64_t zero = 0;
+    uint32_t len32 = (uint32_t)src_len;
+    memcpy(h, &zero, 8);
+    memcpy(h + 8, &len32, 4);
+    if (src_len)
+        memcpy(h + meta, src, src_len);
+    hipStream_t s = t->stream;
+    if (hipMemcpyAsync(d, h, need, hipMemcpyHostToDevice, s) != hipSuccess)
+        return LZO_E_ERROR;
+    if (lzo_mi355x_decoded_length_dev(d + meta, (const uint64_t *)d, (const uint32_t *)(d + 8),
+                                      (uint32_t *)(d + 16), (int32_t *)(d + 20), 1, s) != 0)
+        return LZO_E_ERROR;
+    if (hipMemcpyAsync(h + 16, d + 16, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return LZO_E_ERROR;
+    int32_t st;
+    memcpy(olen, h + 16, 4);
+    memcpy(&st, h + 20, 4);
+    return st;
+}
+
+int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len, unsigned long *dst_len)
+{
+    struct tctx *t = tctx_get();
+    if (!t || src_len > 0xFFFFFFF0u)
+        return LZO_E_ERROR;
+    uint32_t olen = 0;
+    int st = prescan_one(t, src, src_len, &olen);
+    *dst_len = olen;
+    return st;
+}
+
+/* The unchecked entry point never learns the destination size
+ * (mds/itb.c:2951-2964 passes an uninitialised *out_len).  The decoded length
+ * is computed on the GPU first, then the block is decoded into exactly that
+ * many bytes. */
+int lzo1x_decompress(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst, lzo_uintp dst_len,
+                     lzo_voidp wrkmem)
+{
+    (void)wrkmem;
+    struct tctx *t = tctx_get();
+    if (!t || src_len > 0xFFFFFFF0u)
+        return LZO_E_ERROR;
+    uint32_t olen = 0;
+    int st0 = prescan_one(t, src, src_len, &olen);
+    if (st0 == LZO_E_ERROR)
+        return LZO_E_ERROR;
+    const uint8_t *sp[1] = { src };
+    uint8_t *dp[1] = { dst };
+    size_t sl[1] = { src_len }, dl[1] = { olen };
+    int st[1] = { LZO_E_ERROR };
+    int rc = lzo_mi355x_decompress_batch(sp, sl, dp, dl, st, 1);
+    if (rc != LZO_E_OK)
+        return rc;
+    *dst_len = dl[0];
+    return st[0];
+}

@@ -1,0 +1,213 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+The reference codec is /root/reference/lib/minilzo.c compiled in place by
+oracle/Makefile into oracle/_ref/libminilzo_ref.so (never copied into this
+repository).  Every vector below is the reference's own output:
+
+  edge.npz       small inputs (sizes 0..299, boundary sizes, crafted distance
+                 and length cases, a few full 16 KiB blocks) with the exact
+                 bytes lzo1x_1_compress produces from a zero-filled wrkmem
+                 (SURVEY.md finding 3)
+  malformed.npz  damaged/junk streams with lzo1x_decompress_safe's return code,
+                 produced length and produced bytes; inputs are zero padded
+                 past their end, the oracle's convention
+  manifest.json  large batches (configs C1-C4): per-block compressed lengths
+                 and SHA-256 of the concatenated compressed stream and input
+
+Run:  make -C oracle && python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import json
+import os
+import random
+import sys
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, ROOT)
+from pomegranate_amd import synth  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "libminilzo_ref.so")
+OUT = os.path.dirname(os.path.abspath(__file__))
+PAD = 64
+_ulong = ctypes.c_ulong
+
+
+class Ref:
+    def __init__(self, path=REF):
+        self.lib = ctypes.CDLL(path)
+        for fn in ("lzo1x_1_compress", "lzo1x_decompress_safe", "lzo1x_decompress"):
+            f = getattr(self.lib, fn)
+            f.restype = ctypes.c_int
+            f.argtypes = [ctypes.c_void_p, _ulong, ctypes.c_void_p, ctypes.POINTER(_ulong),
+                          ctypes.c_void_p]
+        init = getattr(self.lib, "__lzo_init_v2")   # (no class-private mangling)
+        init.restype = ctypes.c_int
+        assert init(0x2040, 2, 4, 8, 4, 8, 8, 8, 8, 48) == 0
+        self.wrk = ctypes.create_string_buffer(131072)
+
+    def compress(self, data: bytes) -> bytes:
+        n = len(data)
+        src = ctypes.create_string_buffer(data, max(n, 1))
+        out = ctypes.create_string_buffer(n + n // 16 + 67 + 64)
+        olen = _ulong(0)
+        ctypes.memset(self.wrk, 0, 131072)      # zero-filled wrkmem defines the output
+        rc = self.lib.lzo1x_1_compress(src, n, out, ctypes.byref(olen), self.wrk)
+        assert rc == 0
+        return out.raw[: olen.value]
+
+    def decompress_safe(self, comp: bytes, cap: int):
+        src = ctypes.create_string_buffer(comp + b"\0" * PAD, len(comp) + PAD)
+        out = ctypes.create_string_buffer(cap + 16)
+        olen = _ulong(cap)
+        rc = self.lib.lzo1x_decompress_safe(src, len(comp), out, ctypes.byref(olen), None)
+        return rc, out.raw[: olen.value]
+
+
+def pack(blobs):
+    off = np.zeros(len(blobs) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(b) for b in blobs])
+    data = np.frombuffer(b"".join(blobs), dtype=np.uint8) if off[-1] else np.zeros(0, np.uint8)
+    return data, off
+
+
+def edge_cases(ref: Ref):
+    rng = random.Random(2040)
+    names, inputs = [], []
+
+    def add(name, data):
+        names.append(name)
+        inputs.append(bytes(data))
+
+    for model in (synth.RANDOM, synth.ALPHA4, synth.LZLIKE, synth.TEXT):
+        for n in range(300):
+            add(f"size/{synth.MODEL_NAMES[model]}/{n}", synth.block(model, 1000 + n, n))
+    for n in (0, 1, 2, 3, 4, 5, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 31, 32, 33, 34, 237,
+              238, 239, 240, 241, 254, 255, 256, 272, 273, 274, 275, 528, 529):
+        for model in range(6):
+            add(f"boundary/{synth.MODEL_NAMES[model]}/{n}", synth.block(model, 77 + n, n))
+    # match distances around the M2/M3/M4 limits (lib/minilzo.c:2652-2653)
+    for dist in (0x7FF, 0x800, 0x801, 0x802, 0x3FFF, 0x4000, 0x4001, 0x4002, 0xBFFE, 0xBFFF,
+                 0xC000, 0xC001):
+        for ln in (3, 4, 8, 9, 10, 33, 34, 35, 264, 265, 520, 800):
+            x = bytes(rng.getrandbits(8) for _ in range(max(ln, 16) + 8))
+            head = bytes(rng.getrandbits(8) for _ in range(4))
+            tail = bytes(rng.getrandbits(8) for _ in range(30))
+            body = head + x + b"\0" * (dist - len(x)) + x[:ln] + tail
+            add(f"dist/{dist:#x}/len{ln}", body)
+    # match lengths around 8/9, 33/34 and 9+255k (lib/minilzo.c:3094-3145)
+    for ln in (7, 8, 9, 10, 32, 33, 34, 35, 263, 264, 265, 266, 518, 519, 520, 774, 775, 2000):
+        head = bytes(rng.getrandbits(8) for _ in range(10))
+        tail = bytes(rng.getrandbits(8) for _ in range(20))
+        add(f"runs/zeros/{ln}", head + b"\0" * ln + tail)
+        pat = bytes(rng.getrandbits(8) for _ in range(5))
+        add(f"runs/period5/{ln}", head + (pat * (ln // 5 + 2))[: ln + 5] + tail)
+    # literal runs around 3/4, 18/19, 18+255k (lib/minilzo.c:3023-3048)
+    for lit in (1, 2, 3, 4, 5, 17, 18, 19, 20, 272, 273, 274, 528, 529):
+        z = b"\0" * 40
+        add(f"lits/{lit}", z + bytes(rng.getrandbits(8) for _ in range(lit)) + z +
+            bytes(rng.getrandbits(8) for _ in range(lit + 1)) + z)
+    for model in range(6):
+        add(f"full16k/{synth.MODEL_NAMES[model]}", synth.block(model, 4242, 16384))
+    comps = [ref.compress(d) for d in inputs]
+    for d, c in zip(inputs, comps):
+        rc, back = ref.decompress_safe(c, len(d))
+        assert rc == 0 and back == d
+    ind, ino = pack(inputs)
+    zd, zo = pack(comps)
+    np.savez_compressed(os.path.join(OUT, "edge.npz"), names=np.array(names), in_data=ind,
+                        in_off=ino, z_data=zd, z_off=zo)
+    return len(names)
+
+
+def malformed_cases(ref: Ref):
+    rng = random.Random(4190)
+    streams, caps, rcs, outs = [], [], [], []
+    for i in range(900):
+        n = rng.randrange(0, 3000)
+        d = synth.block(i % 6, 9000 + i, n)
+        c = ref.compress(d)
+        mode = i % 7
+        if mode == 0:       # truncated
+            s, cap = c[: rng.randrange(0, len(c))], n
+        elif mode == 1:     # byte damage
+            b = bytearray(c)
+            for _ in range(rng.randrange(1, 4)):
+                b[rng.randrange(len(b))] = rng.getrandbits(8)
+            s, cap = bytes(b), n + rng.randrange(0, 64)
+        elif mode == 2:     # trailing garbage after EOF -> INPUT_NOT_CONSUMED
+            s, cap = c + bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 5))), n
+        elif mode == 3:     # capacity too small -> OUTPUT_OVERRUN
+            s, cap = c, rng.randrange(0, n + 1)
+        elif mode == 4:     # EOF marker removed
+            s, cap = c[:-3], n
+        elif mode == 5:     # junk
+            s = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 80)))
+            cap = rng.randrange(0, 700)
+        else:               # valid, exact capacity
+            s, cap = c, n
+        rc, out = ref.decompress_safe(s, cap)
+        streams.append(s)
+        caps.append(cap)
+        rcs.append(rc)
+        outs.append(out)
+    sd, so = pack(streams)
+    od, oo = pack(outs)
+    np.savez_compressed(os.path.join(OUT, "malformed.npz"), s_data=sd, s_off=so,
+                        cap=np.array(caps, np.int64), rc=np.array(rcs, np.int32),
+                        out_data=od, out_off=oo)
+    return {int(k): rcs.count(k) for k in set(rcs)}
+
+
+def batch_entry(ref: Ref, name, model, seed0, sizes, note):
+    arena, offs, lens = synth.batch(model, seed0, sizes)
+    hz, hi = hashlib.sha256(), hashlib.sha256()
+    zlens = []
+    for b in range(len(lens)):
+        d = arena[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+        z = ref.compress(d)
+        hz.update(z)
+        hi.update(d)
+        zlens.append(len(z))
+    return {"name": name, "model": synth.MODEL_NAMES[model], "model_id": model,
+            "seed0": seed0, "sizes": [int(x) for x in lens] if len(set(map(int, lens))) > 1
+            else int(lens[0]), "nblocks": len(lens), "zlens": zlens,
+            "sha256_input": hi.hexdigest(), "sha256_z": hz.hexdigest(), "note": note}
+
+
+def manifest(ref: Ref):
+    entries = [
+        batch_entry(ref, "C1", synth.RANDOM, 42, [65536] * 1024,
+                    "config C1: 1K random 64 KiB blocks, xorshift64 seed 42+b"),
+        batch_entry(ref, "C2C3", synth.ITB, 0, [65536] * 4096,
+                    "configs C2/C3: 4096 x 64 KiB ITB-like blocks, seed b"),
+        batch_entry(ref, "C4_sample", synth.ITB, 100000, list(synth.mixed_sizes(1024, 4)),
+                    "config C4 sample: 1024 mixed 4-256 KiB ITB-like blocks"),
+        batch_entry(ref, "itb_max", synth.ITB, 500, [536192] * 8,
+                    "largest ITB payload (include/xtable.h:136-144, SURVEY C-5)"),
+        batch_entry(ref, "random_300k", synth.RANDOM, 600, [299106, 300000, 262144, 131077],
+                    "incompressible blocks beyond 256 KiB"),
+    ]
+    for model in range(6):
+        entries.append(batch_entry(ref, f"models64k_{synth.MODEL_NAMES[model]}", model, 7000,
+                                   [65536] * 16, "content-model breadth"))
+    with open(os.path.join(OUT, "manifest.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py",
+                   "reference": "lib/minilzo.c (miniLZO 2.04), zero-filled wrkmem",
+                   "batches": entries}, f, indent=0)
+    return [(e["name"], e["nblocks"]) for e in entries]
+
+
+def main():
+    ref = Ref()
+    print("edge vectors:", edge_cases(ref))
+    print("malformed rc histogram:", malformed_cases(ref))
+    print("manifest:", manifest(ref))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,76 @@
+"""Helpers for GPU tests: pack host blocks into device batches and run the
+device-resident C-ABI (lzo_mi355x_compress_dev / _decompress_dev)."""
+from __future__ import annotations
+
+from typing import List, Sequence
+
+import numpy as np
+
+from pomegranate_amd import lzo
+
+
+def _offsets(sizes, align=16):
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    padded = (sizes + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    off = np.zeros(len(sizes), dtype=np.uint64)
+    if len(sizes) > 1:
+        off[1:] = np.cumsum(padded[:-1])
+    total = int(padded.sum()) if len(sizes) else 0
+    return off, total
+
+
+def device_batch(torch, blocks: Sequence[bytes], dev, shift: int = 0):
+    """Pack blocks (each 16-B aligned + shift) into one HBM arena."""
+    sizes = [len(b) for b in blocks]
+    off, total = _offsets([s + shift for s in sizes])
+    off = off + np.uint64(shift)
+    host = np.zeros(max(total + shift, 1), dtype=np.uint8)
+    for b, o in zip(blocks, off):
+        host[int(o): int(o) + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return lzo.DeviceBatch(t(host), t(off.view(np.int64)),
+                           t(np.asarray(sizes, np.uint32).view(np.int32)))
+
+
+def empty_batch(torch, caps: Sequence[int], dev, fill: int = 0):
+    off, total = _offsets(caps)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    arena = torch.full((max(total, 1),), fill, dtype=torch.uint8, device=dev)
+    return lzo.DeviceBatch(arena, t(off.view(np.int64)),
+                           t(np.asarray(caps, np.uint32).view(np.int32)))
+
+
+def gpu_compress(torch, blocks: Sequence[bytes], dev, shift: int = 0):
+    src = device_batch(torch, blocks, dev, shift)
+    dst = empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
+    n = len(blocks)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    lzo.compress_dev(src, dst, olen, st)
+    torch.cuda.synchronize()
+    return fetch(dst, olen), st.cpu().numpy().tolist()
+
+
+def gpu_decompress(torch, comps: Sequence[bytes], caps: Sequence[int], dev, shift: int = 0):
+    src = device_batch(torch, comps, dev, shift)
+    dst = empty_batch(torch, caps, dev, fill=0x5A)
+    n = len(comps)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    nscr = lzo.decompress_scratch_bytes(n)
+    scratch = torch.empty(max(nscr, 1), dtype=torch.uint8, device=dev) if nscr else None
+    lzo.decompress_dev(src, dst, olen, st, scratch)
+    torch.cuda.synchronize()
+    outs = fetch(dst, olen, cap=caps)
+    return outs, st.cpu().numpy().tolist(), dst
+
+
+def fetch(batch, olen, cap=None) -> List[bytes]:
+    host = batch.arena.cpu().numpy()
+    off = batch.off.cpu().numpy()
+    ol = olen.cpu().numpy().astype(np.int64)
+    res = []
+    for i in range(len(off)):
+        n = int(ol[i]) if cap is None else min(int(ol[i]), int(cap[i]))
+        res.append(host[int(off[i]): int(off[i]) + n].tobytes())
+    return res

@@ -1,0 +1,120 @@
+"""CPU: the drop-in C-ABI library loads and exports every function include/*.h
+declares; the reference call sites compile against include/minilzo.h; without
+a GPU the codec refuses loudly (no CPU fallback)."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+from pomegranate_amd import lzo
+
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def declared_functions():
+    """Function prototypes of include/*.h, via gcc -aux-info."""
+    names = set()
+    for hdr in sorted(os.listdir(INCLUDE)):
+        if not hdr.endswith(".h"):
+            continue
+        aux = f"/tmp/pom_aux_{os.getpid()}_{hdr}.txt"
+        subprocess.run(["gcc", "-fsyntax-only", "-x", "c", f"-aux-info={aux}",
+                        os.path.join(INCLUDE, hdr)], check=True)
+        with open(aux) as f:
+            for line in f:
+                if f"/include/{hdr}:" not in line:
+                    continue
+                m = re.search(r"\*/\s*(?:extern\s+)?[^;(]*?\b(\w+)\s*\(", line)
+                if m:
+                    names.add(m.group(1))
+        os.unlink(aux)
+    return names
+
+
+def test_headers_declare_exactly_the_exports():
+    assert declared_functions() == set(lzo.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(lzo.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", lzo.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    defined = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert declared_functions() <= defined
+
+
+def test_library_has_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readobj", "--sections", lzo.LIB_PATH],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("llvm-readobj unavailable")
+    assert ".hip_fatbin" in out.stdout
+    blob = open(lzo.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_no_oracle_in_product_library():
+    """The product library never links or names the oracle (no CPU fallback)."""
+    blob = open(lzo.LIB_PATH, "rb").read()
+    assert b"oracle" not in blob
+    out = subprocess.run(["ldd", lzo.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out and "minilzo_ref" not in out
+
+
+def test_constants_match_reference_values():
+    assert lzo.LZO1X_1_MEM_COMPRESS == 131072
+    assert lzo.worst_compress(65536) == lzo.load().lzo_mi355x_worst_compress(65536)
+    lib = lzo.load()
+    assert lib.lzo_version() == 0x2040
+    assert lib.lzo_version_string() == b"2.04"
+
+
+def _build_callsite():
+    exe = f"/tmp/pom_itb_callsite_{os.getpid()}"
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", f"-I{INCLUDE}",
+                    os.path.join(ROOT, "tests", "c", "itb_callsite.c"),
+                    f"-L{os.path.dirname(lzo.LIB_PATH)}", "-llzo_mi355x",
+                    f"-Wl,-rpath,{os.path.dirname(lzo.LIB_PATH)}", "-o", exe], check=True)
+    return exe
+
+
+def test_reference_call_sites_compile_against_header():
+    exe = _build_callsite()
+    assert os.path.exists(exe)
+    os.unlink(exe)
+
+
+def _gpu_present():
+    try:
+        import torch
+        return torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_gpu_present(), reason="checks the no-GPU refusal")
+def test_no_gpu_fails_loudly():
+    exe = _build_callsite()
+    r = subprocess.run([exe], capture_output=True, text=True)
+    os.unlink(exe)
+    assert r.returncode == 2
+    assert "no usable GPU" in r.stderr
+    assert lzo.lzo_init() == lzo.LZO_E_ERROR
+    assert lzo.lzo1x_1_compress(b"abc")[0] == lzo.LZO_E_ERROR
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _gpu_present(), reason="needs a GPU")
+def test_reference_call_sites_round_trip_on_gpu():
+    exe = _build_callsite()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    os.unlink(exe)
+    assert r.returncode == 0, r.stderr
+    assert "column data ok" in r.stdout
