@@ -198,6 +198,7 @@ def main():
     zsrc = lzo.DeviceBatch(zarena, zdst.off, zlen)
     lzo.decompress_dev(zsrc, odst, olen, ost, scratch)
     torch.cuda.synchronize()
+    fallback_blocks = int(scratch[:4].view(torch.int32).item()) if scratch is not None else nb
     errors = int((zst != 0).sum().item()) + int((ost != 0).sum().item())
     errors += int((olen != src.length).sum().item()) + (0 if torch.equal(out, src.arena) else 1)
     n_bytes = float(lens.astype(np.float64).sum())
@@ -273,6 +274,7 @@ def main():
         "roundtrip_gibps": round(rt_gibps, 3),
         "compress_kernel_ms": round(comp_kernel * 1e3, 3),
         "errors": errors,
+        "fallback_blocks": fallback_blocks,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         lens_np = np.asarray(lens)

@@ -1,0 +1,656 @@
+// lzo1x_decode_fast.hip -- the throughput LZO1X decoder for MI355X (gfx950).
+//
+// One 64-lane wave per block.  The compressed block is processed in pieces of
+// kPiece input bytes; each piece goes through:
+//
+//  1. PARSE (lane = kSeg-byte input segment).  The LZO1X grammar
+//     (lib/minilzo.c:3308-3699) is a state machine
+//     over instruction starts (pos, state) with state A (top), B (after a
+//     literal run) or C (after 1-3 trailing literals).  Every lane decodes its
+//     segment speculatively from state A and marks the points it visits in
+//     LDS; then each lane walks the TRUE path from its entry (its
+//     predecessor's exit) until it lands on one of its own marks (merged) or
+//     leaves the segment.  Wrong guesses re-synchronise within a few
+//     instructions on real data, so the walk is short; the entry/exit chain is
+//     iterated until no entry changes (lane 0's entry is exact, so this
+//     converges).  Two more walks count and write the ops (literal runs and
+//     matches) of the true path into an LDS op list in stream order.
+//
+//  2. EXECUTE (lane = op, then lane = 4-byte output unit).  64 ops at a time:
+//     a wave prefix sum gives output offsets; the ops are cut into batches
+//     whose match sources all precede the batch (so a batch has no internal
+//     dependency), and each batch's output is produced 256 bytes per step:
+//     every lane finds the op of its output dword through an LDS histogram +
+//     wave scan, gathers the source bytes (input staging / global input for
+//     literals, the LDS output ring or -- beyond the ring -- global output for
+//     matches), and writes the dword to the ring and to HBM.
+//
+// Anything the fast path does not handle exactly (malformed input, lookbehind
+// or capacity errors, op-list overflow, EOF not at the end, misaligned
+// destination...) marks the block for the exact decoder (lzo1x_kernels.hip),
+// which produces the reference's output and LZO_E_* code bit for bit.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lzo_mi355x_kernels.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr uint32_t kSeg = 32;                    // input bytes per lane per piece
+constexpr uint32_t kPiece = kWave * kSeg;        // 2 KiB of compressed input
+constexpr uint32_t kStageMargin = 256;
+constexpr uint32_t kStageBytes = kPiece + kStageMargin;
+constexpr uint32_t kOpMax = 1024;                // ops per piece
+constexpr uint32_t kRing = 16384;                // recent output kept in LDS
+constexpr uint32_t kRingMask = kRing - 1;
+constexpr uint32_t kLitFlag = 0x80000000u;
+constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wrap 32 bits
+constexpr int32_t kFallback = 0x7FFF0001;        // status: exact decoder pending
+
+// parse states (instruction starts)
+constexpr uint32_t ST_A = 0;   // top: t < 16 is a literal run
+constexpr uint32_t ST_B = 1;   // after a literal run: t < 16 is a 3-byte M1 (dist > 0x800)
+constexpr uint32_t ST_C = 2;   // after trailing literals: t < 16 is a 2-byte M1
+constexpr uint32_t ST_F = 3;   // first byte of the stream (lib/minilzo.c:3357)
+constexpr uint32_t kPosEnd = 0xFFFFFFF0u;        // exit marker: EOF reached / dead path
+
+struct __attribute__((aligned(16))) FastLds {
+    uint32_t ring[kRing / 4];
+    uint32_t stage[kStageBytes / 4];
+    uint32_t opL[kOpMax];
+    uint32_t opS[kOpMax];
+    uint32_t wo[kWave + 1];
+    uint32_t ws[kWave + 1];
+    uint32_t hist[kWave + 1];
+    uint8_t marks[kPiece];
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ void wave_order() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, kWave);
+        if (l >= (uint32_t)o)
+            v += t;
+    }
+    return v;
+}
+
+struct Blk {
+    const uint8_t* in;      // compressed block
+    uint32_t z;             // its length
+    uint8_t* out;
+    uint32_t cap;
+    uint32_t P;             // current piece start (input offset)
+    uint32_t staged;        // bytes of input staged at stage[0] (from P)
+    bool err;               // lane-local: true path hit something the fast path refuses
+};
+
+__device__ __forceinline__ uint32_t stage_byte(const FastLds& s, uint32_t i)
+{
+    return (s.stage[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
+}
+
+// Input byte for the parser (0 at or beyond z: oracle convention).
+__device__ __forceinline__ uint32_t rdin(const FastLds& s, const Blk& k, uint32_t pos)
+{
+    if (pos >= k.z)
+        return 0;
+    const uint32_t r = pos - k.P;
+    if (r < k.staged)
+        return stage_byte(s, r);
+    return k.in[pos];
+}
+
+// One instruction from (pos, st).  Produces up to two ops (A: literal run or
+// match; B: trailing literals) and the next point.  `bad` reports reads past
+// the end of the input, literal runs past the end, or an EOF marker that is
+// not the final instruction; `eof` the EOF marker (lib/minilzo.c:3580).
+struct Step {
+    uint32_t pos, st;
+    uint32_t aL, aS;        // op A: length, source (literal: kLitFlag | in pos; match: dist)
+    uint32_t bL, bS;        // op B (bL == 0: none)
+    bool eof, bad;
+};
+
+__device__ __forceinline__ uint32_t read_ext(const FastLds& s, const Blk& k, uint32_t& pos,
+                                             uint32_t base, bool& bad)
+{
+    uint32_t v = 0;
+    while (pos < k.z && rdin(s, k, pos) == 0) {
+        v += 255;
+        pos++;
+    }
+    if (pos >= k.z) {
+        bad = true;
+        return 0;
+    }
+    v += base + rdin(s, k, pos);
+    pos++;
+    return v;
+}
+
+__device__ __forceinline__ Step decode_one(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st)
+{
+    Step r;
+    r.aL = r.bL = 0;
+    r.aS = r.bS = 0;
+    r.eof = r.bad = false;
+    uint32_t t = rdin(s, k, pos);
+    if (pos >= k.z)
+        r.bad = true;
+    if (st == ST_F) {
+        if (t > 17) {
+            const uint32_t n = t - 17;
+            r.aL = n;
+            r.aS = kLitFlag | (pos + 1);
+            r.pos = pos + 1 + n;
+            r.st = n < 4 ? ST_C : ST_B;
+            if (r.pos > k.z)
+                r.bad = true;
+            return r;
+        }
+        st = ST_A;
+    }
+    uint32_t L, d;
+    if (t < 16 && st == ST_A) {                       // literal run, :3367-3414
+        pos++;
+        if (t == 0)
+            t = read_ext(s, k, pos, 15, r.bad);
+        const uint32_t n = t + 3;
+        r.aL = n;
+        r.aS = kLitFlag | pos;
+        r.pos = pos + n;
+        r.st = ST_B;
+        if (r.pos > k.z || r.pos < pos)
+            r.bad = true;
+        return r;
+    }
+    if (t < 16) {                                     // M1 forms, :3416-3443 / :3600-3612
+        d = (st == ST_B ? 0x801u : 1u) + (t >> 2) + (rdin(s, k, pos + 1) << 2);
+        L = st == ST_B ? 3u : 2u;
+        pos += 2;
+    } else if (t >= 64) {                             // M2
+        d = 1 + ((t >> 2) & 7) + (rdin(s, k, pos + 1) << 3);
+        L = (t >> 5) + 1;
+        pos += 2;
+    } else if (t >= 32) {                             // M3
+        L = t & 31;
+        pos++;
+        if (L == 0)
+            L = read_ext(s, k, pos, 31, r.bad);
+        L += 2;
+        d = 1 + ((rdin(s, k, pos) | (rdin(s, k, pos + 1) << 8)) >> 2);
+        pos += 2;
+    } else {                                          // M4 / EOF
+        uint32_t dd = (t & 8) << 11;
+        L = t & 7;
+        pos++;
+        if (L == 0)
+            L = read_ext(s, k, pos, 7, r.bad);
+        L += 2;
+        dd += (rdin(s, k, pos) | (rdin(s, k, pos + 1) << 8)) >> 2;
+        pos += 2;
+        if (dd == 0) {
+            r.eof = true;
+            r.pos = pos;
+            r.st = ST_A;
+            if (pos != k.z)
+                r.bad = true;                         // INPUT_NOT_CONSUMED / OVERRUN
+            return r;
+        }
+        d = dd + 0x4000;
+    }
+    if (pos > k.z)
+        r.bad = true;
+    r.aL = L;
+    r.aS = d;
+    const uint32_t tl = rdin(s, k, pos - 2) & 3;      // match_done, :3650-3653
+    if (tl) {
+        r.bL = tl;
+        r.bS = kLitFlag | pos;
+        pos += tl;
+        r.st = ST_C;
+        if (pos > k.z)
+            r.bad = true;
+    } else
+        r.st = ST_A;
+    r.pos = pos;
+    return r;
+}
+
+// Output byte / dword helpers ------------------------------------------------
+__device__ __forceinline__ uint32_t ring_byte(const FastLds& s, uint32_t y)
+{
+    const uint32_t i = y & kRingMask;
+    return (s.ring[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh)
+{
+    // bytes [sh, sh+4) of the 8-byte little-endian value hi:lo
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+}
+
+__device__ __forceinline__ uint32_t ring_dword(const FastLds& s, uint32_t y)
+{
+    const uint32_t i = y & kRingMask;
+    const uint32_t w0 = s.ring[i >> 2];
+    const uint32_t w1 = s.ring[((i >> 2) + 1) & (kRingMask >> 2)];
+    return funnel(w0, w1, i & 3u);
+}
+
+// 4 bytes at an arbitrary global address via two aligned dword loads (an
+// aligned dword that overlaps valid bytes never leaves their page).
+template <bool NT>
+__device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t w0, w1 = 0;
+    if (NT) {
+        w0 = __builtin_nontemporal_load(q);
+        if (sh)
+            w1 = __builtin_nontemporal_load(q + 1);
+    } else {
+        w0 = q[0];
+        if (sh)
+            w1 = q[1];
+    }
+    return sh ? funnel(w0, w1, sh) : w0;
+}
+
+__device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t w = __builtin_nontemporal_load((const uint32_t*)(a & ~(uintptr_t)3));
+    return (w >> (8u * (uint32_t)(a & 3))) & 0xFFu;
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+    uint32_t* __restrict__ fallback, uint32_t nblocks)
+{
+    __shared__ FastLds S;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t l = lane_id();
+    Blk k;
+    k.in = src + src_off[b];
+    k.z = src_len[b];
+    k.out = dst + dst_off[b];
+    k.cap = dst_cap[b];
+    k.err = false;
+    k.P = 0;
+    k.staged = 0;
+
+    // The exact decoder takes: misaligned destinations, empty or huge blocks
+    // (lengths up to 255 * z must not wrap 32 bits).
+    bool refuse = ((uintptr_t)k.out & 3) != 0 || k.z >= (1u << 24) || k.z == 0;
+    uint32_t entry_pos = 0, entry_st = ST_F;   // true entry of the current piece
+    uint32_t carry = 0;                        // output produced so far
+    bool done = false;                         // EOF consumed
+
+    while (!refuse && !done) {
+        // Skip pieces in which no instruction starts (inside a long literal run).
+        if (entry_pos >= k.P + kPiece)
+            k.P = entry_pos - (entry_pos % kPiece);
+        if (k.P >= k.z) {                      // ran off the end without EOF
+            refuse = true;
+            break;
+        }
+        // ---- stage the piece's input ------------------------------------
+        {
+            const uint32_t avail = k.z - k.P;
+            k.staged = avail < kStageBytes ? avail : kStageBytes;
+            const uint8_t* base = k.in + k.P;
+            for (uint32_t i = l * 4; i < kStageBytes; i += kWave * 4) {
+                uint32_t w = 0;
+                if (i < k.staged) {
+                    if (i + 4 <= k.staged)
+                        w = global_dword<false>(base + i);
+                    else
+                        for (uint32_t j = 0; j < k.staged - i; j++)
+                            w |= (uint32_t)base[i + j] << (8 * j);
+                }
+                S.stage[i >> 2] = w;
+            }
+            for (uint32_t i = l * 4; i < kPiece; i += kWave * 4)
+                *(uint32_t*)&S.marks[i] = 0;
+        }
+        wave_order();
+        const uint32_t c0 = k.P + l * kSeg;            // this lane's segment
+        const uint32_t c1 = c0 + kSeg;
+
+        // ---- pass 1: speculative walk, mark visited points ------------------
+        uint32_t xpos, xst;
+        {
+            uint32_t pos = c0, st = ST_A;
+            if (l == 0) {
+                pos = entry_pos;
+                st = entry_st;
+            }
+            bool dead = false;
+            if (c1 <= entry_pos)
+                pos = c1;                              // segment inside the entry's run: skip
+            while (pos < c1 && pos < k.z) {
+                S.marks[pos - k.P] = (uint8_t)(st + 1);
+                const Step r = decode_one(S, k, pos, st);
+                if (r.bad || r.eof) {
+                    dead = true;
+                    break;
+                }
+                pos = r.pos;
+                st = r.st;
+            }
+            xpos = dead ? kPosEnd : pos;
+            xst = dead ? 0u : st;
+            if (pos >= k.z && !dead)
+                xpos = kPosEnd;                        // walked off the input: dead too
+        }
+        wave_order();
+
+        // ---- resolve true entries: walk until merged into own marks ----------
+        uint32_t epos = __shfl_up(xpos, 1, kWave), est = __shfl_up(xst, 1, kWave);
+        if (l == 0) {
+            epos = entry_pos;
+            est = entry_st;
+        }
+        uint32_t fpos = 0, fst = 0;
+        for (int iter = 0; iter < kWave + 1; iter++) {
+            uint32_t pos = epos, st = est;
+            bool merged = false, dead = false;
+            while (pos < c1) {
+                if (pos >= k.z) {
+                    dead = true;
+                    break;
+                }
+                if (pos >= c0 && S.marks[pos - k.P] == st + 1) {
+                    merged = true;
+                    break;
+                }
+                const Step r = decode_one(S, k, pos, st);
+                if (r.bad || r.eof) {
+                    dead = true;                       // true-path EOF/errors seen in pass 3
+                    break;
+                }
+                pos = r.pos;
+                st = r.st;
+            }
+            if (merged) {
+                fpos = xpos;
+                fst = xst;
+            } else if (dead) {
+                fpos = kPosEnd;
+                fst = 0;
+            } else {
+                fpos = pos;
+                fst = st;
+            }
+            uint32_t npos = __shfl_up(fpos, 1, kWave), nst = __shfl_up(fst, 1, kWave);
+            if (l == 0) {
+                npos = entry_pos;
+                nst = entry_st;
+            }
+            const bool changed = npos != epos || nst != est;
+            if (!wave_ballot(changed))
+                break;
+            epos = npos;
+            est = nst;
+        }
+        // epos/est: true entry of this lane's segment (kPosEnd: none)
+
+        // ---- pass 3: count ops of the true path ------------------------------
+        uint32_t nops = 0;
+        bool lane_eof = false;
+        {
+            uint32_t pos = epos, st = est;
+            while (pos < c1) {
+                const Step r = decode_one(S, k, pos, st);
+                if (r.bad) {
+                    k.err = true;
+                    break;
+                }
+                if (r.eof) {                           // EOF carries no op
+                    lane_eof = true;
+                    break;
+                }
+                if (r.aL > kMaxOpLen || r.bL > kMaxOpLen) {
+                    k.err = true;
+                    break;
+                }
+                nops += (r.aL ? 1u : 0u) + (r.bL ? 1u : 0u);
+                pos = r.pos;
+                st = r.st;
+            }
+        }
+        if (wave_ballot(k.err)) {
+            refuse = true;
+            break;
+        }
+        const uint32_t incl = wave_incl_scan(nops);
+        const uint32_t total_ops = lane_read(incl, kWave - 1);
+        if (total_ops > kOpMax) {
+            refuse = true;
+            break;
+        }
+        // ---- pass 4: write the ops --------------------------------------------
+        {
+            uint32_t w = incl - nops;
+            uint32_t pos = epos, st = est;
+            while (pos < c1) {
+                const Step r = decode_one(S, k, pos, st);
+                if (r.eof)
+                    break;
+                if (r.aL) {
+                    S.opL[w] = r.aL;
+                    S.opS[w] = r.aS;
+                    w++;
+                }
+                if (r.bL) {
+                    S.opL[w] = r.bL;
+                    S.opS[w] = r.bS;
+                    w++;
+                }
+                pos = r.pos;
+                st = r.st;
+            }
+        }
+        wave_order();
+        const uint64_t eofm = wave_ballot(lane_eof);
+        // next piece's entry: exit of the last lane's true walk
+        {
+            const uint32_t lastp = lane_read(fpos, kWave - 1);
+            const uint32_t lasts = lane_read(fst, kWave - 1);
+            entry_pos = lastp;
+            entry_st = lasts;
+        }
+        if (eofm)
+            done = true;
+        else if (entry_pos == kPosEnd) {               // dead without EOF
+            refuse = true;
+            break;
+        }
+
+        // ---- execute the piece's ops, 64 at a time ----------------------------
+        for (uint32_t w0 = 0; w0 < total_ops && !refuse; w0 += kWave) {
+            const uint32_t nwin = total_ops - w0 < (uint32_t)kWave ? total_ops - w0 : (uint32_t)kWave;
+            uint32_t L = 0, Sv = 0;
+            if (l < nwin) {
+                L = S.opL[w0 + l];
+                Sv = S.opS[w0 + l];
+            }
+            const uint32_t inc = wave_incl_scan(L);
+            const uint32_t o = carry + inc - L;
+            const uint32_t wtotal = lane_read(inc, kWave - 1);
+            if (carry + wtotal < carry || carry + wtotal > k.cap) {
+                refuse = true;                         // OUTPUT_OVERRUN (or wrap)
+                break;
+            }
+            const bool lit = (Sv & kLitFlag) != 0;
+            const uint32_t dist = Sv;
+            bool lb = l < nwin && !lit && dist > o;      // LOOKBEHIND_OVERRUN
+            if (wave_ballot(lb)) {
+                refuse = true;
+                break;
+            }
+            // end of each match's source range (periodic copies read only [o-d, o))
+            const uint32_t send = lit ? 0u : o - dist + (dist < L ? dist : L);
+            S.wo[l] = o;
+            S.ws[l] = Sv;
+            if (l == 0)
+                S.wo[kWave] = carry + wtotal;
+            wave_order();
+            uint32_t s = 0;
+            while (s < nwin) {
+                const uint32_t os = lane_read(o, s);
+                const bool brk = l > s && l < nwin && !lit && send > os;
+                const uint64_t bm = wave_ballot(brk);
+                const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nwin;
+                const uint32_t oe = e < (uint32_t)kWave ? S.wo[e] : carry + wtotal;
+                // ---- batch [s, e): output [os, oe) -------------------------
+                const uint32_t base = os & ~3u;
+                const uint32_t units = (oe - base + 3) >> 2;
+                for (uint32_t u0 = 0; u0 < units; u0 += kWave) {
+                    // op of each lane's first byte: histogram of op starts + scan
+                    S.hist[l] = 0;
+                    wave_order();
+                    if (l >= s && l < e) {
+                        const uint32_t c = (o - base + 3) >> 2;   // first unit starting at/after o
+                        const int32_t slot = (int32_t)c - (int32_t)u0;
+                        if (slot < kWave)
+                            atomicAdd(&S.hist[slot < 0 ? 0 : slot], 1u);
+                    }
+                    wave_order();
+                    const uint32_t cnt = wave_incl_scan(S.hist[l]);
+                    const uint32_t u = u0 + l;
+                    if (u < units) {
+                        const uint32_t x = base + 4 * u;
+                        // op index j of byte x (s-1: belongs to an earlier batch)
+                        int32_t j = (int32_t)s + (int32_t)cnt - 1;
+                        uint32_t val = 0;
+                        const uint32_t step_end = base + 4 * (u0 + kWave);
+                        const uint32_t nxt_o = (j + 1 < (int32_t)e) ? S.wo[j + 1] : oe;
+                        bool fast = j >= (int32_t)s && x + 4 <= nxt_o && x + 4 <= oe;
+                        if (fast) {
+                            const uint32_t oj = S.wo[j];
+                            const uint32_t sj = S.ws[j];
+                            const uint32_t r = x - oj;
+                            if (sj & kLitFlag) {
+                                const uint32_t ip = (sj & ~kLitFlag) + r;
+                                const uint32_t rel = ip - k.P;
+                                if (rel + 4 <= k.staged) {
+                                    const uint32_t w0s = S.stage[rel >> 2];
+                                    const uint32_t w1s = S.stage[((rel >> 2) + 1) < kStageBytes / 4 ? (rel >> 2) + 1 : (rel >> 2)];
+                                    val = funnel(w0s, w1s, rel & 3u);
+                                } else
+                                    val = global_dword<false>(k.in + ip);
+                            } else {
+                                const uint32_t d = sj;
+                                uint32_t rr = r;
+                                if (rr >= d)
+                                    rr %= d;
+                                if (rr + 4 <= d) {
+                                    const uint32_t y = oj - d + rr;
+                                    if (y + kRing >= step_end + 4)
+                                        val = ring_dword(S, y);
+                                    else {
+                                        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): own stores landed
+                                        val = global_dword<true>(k.out + y);
+                                    }
+                                } else
+                                    fast = false;
+                            }
+                        }
+                        if (!fast) {
+                            // byte-serial assembly; ops may change inside the dword
+                            int32_t jj = j;
+                            for (uint32_t q = 0; q < 4; q++) {
+                                const uint32_t xb = x + q;
+                                while (jj + 1 < (int32_t)e && S.wo[jj + 1] <= xb)
+                                    jj++;
+                                uint32_t bv = 0;
+                                if (xb < os) {
+                                    bv = ring_byte(S, xb);            // earlier batch's byte
+                                } else if (xb < oe && jj >= (int32_t)s) {
+                                    const uint32_t oj = S.wo[jj];
+                                    const uint32_t sj = S.ws[jj];
+                                    const uint32_t r = xb - oj;
+                                    if (sj & kLitFlag) {
+                                        const uint32_t ip = (sj & ~kLitFlag) + r;
+                                        const uint32_t rel = ip - k.P;
+                                        bv = rel < k.staged ? stage_byte(S, rel) : k.in[ip];
+                                    } else {
+                                        const uint32_t d = sj;
+                                        const uint32_t y = oj - d + (r >= d ? r % d : r);
+                                        if (y + kRing >= step_end + 4)
+                                            bv = ring_byte(S, y);
+                                        else {
+                                            __builtin_amdgcn_s_waitcnt(0x0F70);
+                                            bv = global_byte_nt(k.out + y);
+                                        }
+                                    }
+                                }
+                                val |= bv << (8 * q);
+                            }
+                        }
+                        S.ring[(x & kRingMask) >> 2] = val;
+                        // Bytes past oe are not known yet: the next batch's first
+                        // unit stores the whole dword.  Nothing past oe (<= cap).
+                        if (x + 4 <= oe)
+                            *(uint32_t*)(k.out + x) = val;
+                        else
+                            for (uint32_t q = 0; q < 4 && x + q < oe; q++)
+                                k.out[x + q] = (uint8_t)(val >> (8 * q));
+                    }
+                    wave_order();
+                }
+                s = e;
+            }
+            carry += wtotal;
+            wave_order();
+        }
+        k.P += kPiece;
+    }
+
+    if (l == 0) {
+        if (refuse) {
+            status[b] = kFallback;
+            const uint32_t at = atomicAdd(&fallback[0], 1u);
+            fallback[1 + at] = b;
+        } else {
+            out_len[b] = carry;
+            status[b] = 0;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint64_t* src_off,
+                                                 const uint32_t* src_len, uint8_t* dst,
+                                                 const uint64_t* dst_off, const uint32_t* dst_cap,
+                                                 uint32_t* out_len, int32_t* status,
+                                                 uint32_t* fallback, uint32_t nblocks,
+                                                 hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_decode_fast_kernel, dim3(nblocks), dim3(kWave), 0, stream, src,
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
+                       nblocks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

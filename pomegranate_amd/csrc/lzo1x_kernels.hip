@@ -310,21 +310,17 @@ __device__ int dec_run(Dec<WRITE>& d)
 }
 
 template <bool WRITE>
-__global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
-    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-    const uint32_t* __restrict__ only, uint32_t nblocks)
+__device__ void decode_exact_block(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+                                   const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+                                   const uint64_t* __restrict__ dst_off,
+                                   const uint32_t* __restrict__ dst_cap,
+                                   uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+                                   uint8_t* ring, uint32_t b)
 {
-    __shared__ uint8_t ring[WRITE ? kRing : 4];
-    const uint32_t b = only ? only[blockIdx.x] : blockIdx.x;
-    if (b >= nblocks)
-        return;
     Dec<WRITE> d;
     d.W.in = src + src_off[b];
     d.W.len = src_len[b];
-    d.W.r0 = -((int64_t)1 << 40);     // empty window: the first read loads it
+    d.W.r0 = -((int64_t)1 << 40);      // empty window: the first read loads it
     d.W.w = 0;
     d.ring = ring;
     d.out = dst ? dst + dst_off[b] : nullptr;
@@ -335,6 +331,32 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
     if (lane_id() == 0) {
         out_len[b] = d.op;
         status[b] = rc;
+    }
+}
+
+// fb == nullptr: grid entry b decodes block b.  Otherwise fb[0] blocks listed
+// at fb[1..] (the fast decoder's refusals) are decoded grid-stride.
+template <bool WRITE>
+__global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+    const uint32_t* __restrict__ fb, uint32_t nblocks)
+{
+    __shared__ uint8_t ring[WRITE ? kRing : 4];
+    if (!fb) {
+        if (blockIdx.x < nblocks)
+            decode_exact_block<WRITE>(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
+                                      status, ring, blockIdx.x);
+        return;
+    }
+    const uint32_t count = fb[0];
+    for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+        const uint32_t b = fb[1 + i];
+        if (b < nblocks)
+            decode_exact_block<WRITE>(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
+                                      status, ring, b);
     }
 }
 
@@ -693,13 +715,13 @@ extern "C" int lzo_mi355x_launch_decompress_exact(const uint8_t* src, const uint
                                                   const uint32_t* src_len, uint8_t* dst,
                                                   const uint64_t* dst_off, const uint32_t* dst_cap,
                                                   uint32_t* out_len, int32_t* status,
-                                                  const uint32_t* only, uint32_t ngrid,
+                                                  const uint32_t* fb, uint32_t ngrid,
                                                   uint32_t nblocks, hipStream_t stream)
 {
     if (ngrid == 0)
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_exact_kernel<true>, dim3(ngrid), dim3(kWave), 0, stream, src,
-                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, only, nblocks);
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fb, nblocks);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -152,20 +152,33 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
 
 size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
 {
-    (void)nblocks;
-    return 0;
+    return 4 * ((size_t)nblocks + 1);
 }
 
+/* Fast decoder over the whole batch, then the exact decoder over the blocks
+ * it refused (malformed input, capacity/lookbehind errors, pathological
+ * streams).  Without scratch every block takes the exact decoder. */
 int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
                               const uint32_t *src_len, uint8_t *dst,
                               const uint64_t *dst_off, const uint32_t *dst_cap,
                               uint32_t *out_len, int32_t *status, uint32_t nblocks,
                               void *scratch, void *stream)
 {
-    (void)scratch;
+    hipStream_t s = (hipStream_t)stream;
+    if (nblocks == 0)
+        return 0;
+    if (!scratch)
+        return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
+                                                  out_len, status, NULL, nblocks, nblocks, s);
+    uint32_t *fb = (uint32_t *)scratch;
+    if (hipMemsetAsync(fb, 0, 4, s) != hipSuccess)
+        return -1;
+    if (lzo_mi355x_launch_decompress_fast(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
+                                          status, fb, nblocks, s) != 0)
+        return -1;
+    const uint32_t ngrid = nblocks < 512 ? nblocks : 512;
     return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
-                                              out_len, status, NULL, nblocks, nblocks,
-                                              (hipStream_t)stream);
+                                              out_len, status, fb, ngrid, nblocks, s);
 }
 
 int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,
@@ -185,7 +198,7 @@ int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,
 struct layout {
     size_t nb;
     size_t o_srcoff, o_dstoff, o_srclen, o_dstcap, o_outlen, o_status;
-    size_t o_src, o_dst, total;
+    size_t o_src, o_dst, o_scr, total;
     size_t src_bytes, dst_bytes;
 };
 
@@ -211,6 +224,8 @@ static void layout_make(struct layout *L, size_t nb, const size_t *src_len, cons
     o += ALIGN_UP(s, 256);
     L->o_dst = o;
     o += ALIGN_UP(d, 256);
+    L->o_scr = o;
+    o += ALIGN_UP(lzo_mi355x_decompress_scratch((uint32_t)nb), 256);
     L->total = o;
 }
 
@@ -257,7 +272,7 @@ static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
     if (kind == OP_COMPRESS)
         rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, s);
     else
-        rc = lzo_mi355x_decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, NULL, s);
+        rc = lzo_mi355x_decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, s);
     if (rc != 0)
         return -1;
     if (hipMemcpyAsync(h + L->o_outlen, d + L->o_outlen, 8 * L->nb, hipMemcpyDeviceToHost, s) !=
