@@ -5,25 +5,28 @@
 //
 //  1. PARSE (lane = kSeg-byte input segment).  The LZO1X grammar
 //     (lib/minilzo.c:3308-3699) is a state machine
-//     over instruction starts (pos, state) with state A (top), B (after a
-//     literal run) or C (after 1-3 trailing literals).  Every lane decodes its
-//     segment speculatively from state A and marks the points it visits in
-//     LDS; then each lane walks the TRUE path from its entry (its
-//     predecessor's exit) until it lands on one of its own marks (merged) or
-//     leaves the segment.  Wrong guesses re-synchronise within a few
-//     instructions on real data, so the walk is short; the entry/exit chain is
-//     iterated until no entry changes (lane 0's entry is exact, so this
-//     converges).  Two more walks count and write the ops (literal runs and
-//     matches) of the true path into an LDS op list in stream order.
+//     over instruction starts (pos, state), state A (top), B (after a literal
+//     run) or C (after 1-3 trailing literals).  Every lane decodes
+//     speculatively from kLook bytes before its segment (state A, restarting
+//     one byte later whenever the guess runs into an impossible instruction)
+//     and marks the points it visits inside its segment.  Each lane then walks
+//     the TRUE path from its entry (its predecessor's exit) until it lands on
+//     one of its own marks (merged) or leaves the segment; the entry/exit
+//     chain is iterated until no entry changes (lane 0's entry is exact, so
+//     this converges; on real data speculation re-synchronises within a few
+//     instructions and one round suffices).  Two more walks count and write
+//     the ops (literal runs and matches) of the true path into an LDS op list
+//     in stream order.
 //
 //  2. EXECUTE (lane = op, then lane = 4-byte output unit).  64 ops at a time:
-//     a wave prefix sum gives output offsets; the ops are cut into batches
-//     whose match sources all precede the batch (so a batch has no internal
-//     dependency), and each batch's output is produced 256 bytes per step:
-//     every lane finds the op of its output dword through an LDS histogram +
-//     wave scan, gathers the source bytes (input staging / global input for
-//     literals, the LDS output ring or -- beyond the ring -- global output for
-//     matches), and writes the dword to the ring and to HBM.
+//     a DPP prefix sum gives output offsets; the ops are cut into batches
+//     whose match sources all precede the batch (no dependency inside a
+//     batch), and each batch's output is produced 256 bytes per step: op
+//     starts are flagged per byte in LDS, a DPP scan of the per-unit flag
+//     counts gives every byte its op, and each lane gathers its 4 bytes
+//     (input staging / global input for literals; the LDS output ring or,
+//     beyond the ring, the already-stored HBM output for matches) and writes
+//     the dword to the ring and to HBM.
 //
 // Anything the fast path does not handle exactly (malformed input, lookbehind
 // or capacity errors, op-list overflow, EOF not at the end, misaligned
@@ -37,12 +40,12 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr uint32_t kSeg = 32;                    // input bytes per lane per piece
-constexpr uint32_t kPiece = kWave * kSeg;        // 2 KiB of compressed input
-constexpr uint32_t kStageMargin = 256;
-constexpr uint32_t kStageBytes = kPiece + kStageMargin;
-constexpr uint32_t kOpMax = 1024;                // ops per piece
-constexpr uint32_t kRing = 16384;                // recent output kept in LDS
+constexpr uint32_t kSeg = 16;                    // input bytes per lane per piece
+constexpr uint32_t kLook = 24;                   // speculative lead-in before a segment
+constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
+constexpr uint32_t kStageBytes = kPiece + 512;
+constexpr uint32_t kOpMax = 512;                 // ops per piece
+constexpr uint32_t kRing = 8192;                 // recent output kept in LDS
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kLitFlag = 0x80000000u;
 constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wrap 32 bits
@@ -60,9 +63,9 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t stage[kStageBytes / 4];
     uint32_t opL[kOpMax];
     uint32_t opS[kOpMax];
-    uint32_t wo[kWave + 1];
-    uint32_t ws[kWave + 1];
-    uint32_t hist[kWave + 1];
+    uint32_t wo[kWave + 4];
+    uint32_t ws[kWave + 4];
+    uint32_t flags[kWave];
     uint8_t marks[kPiece];
 };
 
@@ -71,16 +74,24 @@ __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return _
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ void wave_order() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
 
+// Inclusive prefix sum over the wave: DPP row shifts inside each 16-lane row,
+// then the row totals via readlane (no LDS round trip).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 {
-    const uint32_t l = lane_id();
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, kWave);
-        if (l >= (uint32_t)o)
-            v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    const uint32_t r0 = lane_read(v, 15), r1 = lane_read(v, 31), r2 = lane_read(v, 47);
+    const uint32_t row = lane_id() >> 4;
+    v += (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
     return v;
+}
+
+__device__ __forceinline__ uint32_t shift_up1(uint32_t v, uint32_t fill)
+{
+    const uint32_t u = (uint32_t)__shfl_up((int)v, 1, kWave);
+    return lane_id() == 0 ? fill : u;
 }
 
 struct Blk {
@@ -90,7 +101,6 @@ struct Blk {
     uint32_t cap;
     uint32_t P;             // current piece start (input offset)
     uint32_t staged;        // bytes of input staged at stage[0] (from P)
-    bool err;               // lane-local: true path hit something the fast path refuses
 };
 
 __device__ __forceinline__ uint32_t stage_byte(const FastLds& s, uint32_t i)
@@ -226,7 +236,7 @@ __device__ __forceinline__ Step decode_one(const FastLds& s, const Blk& k, uint3
     return r;
 }
 
-// Output byte / dword helpers ------------------------------------------------
+// Output / input byte helpers -------------------------------------------------
 __device__ __forceinline__ uint32_t ring_byte(const FastLds& s, uint32_t y)
 {
     const uint32_t i = y & kRingMask;
@@ -235,7 +245,6 @@ __device__ __forceinline__ uint32_t ring_byte(const FastLds& s, uint32_t y)
 
 __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh)
 {
-    // bytes [sh, sh+4) of the 8-byte little-endian value hi:lo
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
 }
 
@@ -247,8 +256,16 @@ __device__ __forceinline__ uint32_t ring_dword(const FastLds& s, uint32_t y)
     return funnel(w0, w1, i & 3u);
 }
 
+__device__ __forceinline__ uint32_t stage_dword(const FastLds& s, uint32_t r)
+{
+    const uint32_t w0 = s.stage[r >> 2];
+    const uint32_t w1 = (r & 3u) ? s.stage[(r >> 2) + 1] : 0u;
+    return funnel(w0, w1, r & 3u);
+}
+
 // 4 bytes at an arbitrary global address via two aligned dword loads (an
-// aligned dword that overlaps valid bytes never leaves their page).
+// aligned dword that overlaps valid bytes never leaves their page).  NT: L2
+// served (the vector L1 is not coherent with this wave's earlier stores).
 template <bool NT>
 __device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
 {
@@ -275,15 +292,44 @@ __device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
     return (w >> (8u * (uint32_t)(a & 3))) & 0xFFu;
 }
 
+// A far match source y (beyond the ring) was stored >= (kRing-256)/256 = 31
+// steps ago, one or more global stores per step: once at most 16 of this
+// wave's vector-memory operations are outstanding, that store has landed in
+// L2 (vmcnt retires in issue order), and the L2-served load below sees it.
+__device__ __forceinline__ void far_wait() { __builtin_amdgcn_s_waitcnt(0x4F70); }   // vmcnt(16)
+
+__device__ __forceinline__ uint32_t match_src(uint32_t oj, uint32_t d, uint32_t L, uint32_t r)
+{
+    // byte-serial overlap semantics: out[o + r] = out[o - d + (r mod d)]
+    const uint32_t rr = (d < L && r >= d) ? r % d : r;
+    return oj - d + rr;
+}
+
+// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums go to
+// stamps[b * 8 + phase]; no output value depends on them.
+enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_ITER };
+
 // ---------------------------------------------------------------------------
+template <bool STAMPS>
 __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-    uint32_t* __restrict__ fallback, uint32_t nblocks)
+    uint32_t* __restrict__ fallback, uint32_t nblocks, uint64_t* __restrict__ stamps)
 {
     __shared__ FastLds S;
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+#define STAMP(ph)                                                   \
+    do {                                                            \
+        if (STAMPS) {                                               \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+            acc[ph] += now_ - tmark;                                \
+            tmark = now_;                                           \
+        }                                                           \
+    } while (0)
+
     const uint32_t b = blockIdx.x;
     if (b >= nblocks)
         return;
@@ -293,7 +339,6 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
     k.z = src_len[b];
     k.out = dst + dst_off[b];
     k.cap = dst_cap[b];
-    k.err = false;
     k.P = 0;
     k.staged = 0;
 
@@ -312,65 +357,66 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
             refuse = true;
             break;
         }
-        // ---- stage the piece's input ------------------------------------
+        // ---- stage the piece's input --------------------------------------
         {
             const uint32_t avail = k.z - k.P;
             k.staged = avail < kStageBytes ? avail : kStageBytes;
             const uint8_t* base = k.in + k.P;
             for (uint32_t i = l * 4; i < kStageBytes; i += kWave * 4) {
                 uint32_t w = 0;
-                if (i < k.staged) {
-                    if (i + 4 <= k.staged)
-                        w = global_dword<false>(base + i);
-                    else
-                        for (uint32_t j = 0; j < k.staged - i; j++)
-                            w |= (uint32_t)base[i + j] << (8 * j);
-                }
+                if (i + 4 <= k.staged)
+                    w = global_dword<false>(base + i);
+                else
+                    for (uint32_t j = i; j < k.staged; j++)
+                        w |= (uint32_t)base[j] << (8 * (j - i));
                 S.stage[i >> 2] = w;
             }
             for (uint32_t i = l * 4; i < kPiece; i += kWave * 4)
                 *(uint32_t*)&S.marks[i] = 0;
         }
         wave_order();
+        STAMP(PH_STAGE);
         const uint32_t c0 = k.P + l * kSeg;            // this lane's segment
         const uint32_t c1 = c0 + kSeg;
 
-        // ---- pass 1: speculative walk, mark visited points ------------------
-        uint32_t xpos, xst;
-        {
-            uint32_t pos = c0, st = ST_A;
-            if (l == 0) {
+        // ---- pass 1: speculative walk, mark visited points -------------------
+        // A mark is (state + 1) | (gen << 2); gen counts this lane's restarts,
+        // and only marks of the final generation lie on the path that really
+        // reaches xpos (a restart breaks the chain).
+        uint32_t xpos, xst, xgen = 0;
+        if (c1 <= entry_pos) {                         // no instruction starts here
+            xpos = entry_pos;
+            xst = entry_st;
+        } else {
+            uint32_t pos = c0 >= k.P + kLook ? c0 - kLook : k.P;
+            if (pos < entry_pos)
                 pos = entry_pos;
-                st = entry_st;
-            }
-            bool dead = false;
-            if (c1 <= entry_pos)
-                pos = c1;                              // segment inside the entry's run: skip
+            uint32_t st = pos == entry_pos ? entry_st : ST_A;
+            uint32_t gen = 0;
             while (pos < c1 && pos < k.z) {
-                S.marks[pos - k.P] = (uint8_t)(st + 1);
+                if (pos >= c0)
+                    S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 2));
                 const Step r = decode_one(S, k, pos, st);
-                if (r.bad || r.eof) {
-                    dead = true;
-                    break;
+                if (r.bad || r.eof) {                  // impossible guess: restart later
+                    pos++;
+                    st = ST_A;
+                    gen = gen < 63 ? gen + 1 : 63;
+                    continue;
                 }
                 pos = r.pos;
                 st = r.st;
             }
-            xpos = dead ? kPosEnd : pos;
-            xst = dead ? 0u : st;
-            if (pos >= k.z && !dead)
-                xpos = kPosEnd;                        // walked off the input: dead too
+            xpos = pos >= k.z ? kPosEnd : pos;
+            xst = st;
+            xgen = gen < 63 ? gen : 0xFFu;             // saturated: never merge
         }
         wave_order();
+        STAMP(PH_PASS1);
 
         // ---- resolve true entries: walk until merged into own marks ----------
-        uint32_t epos = __shfl_up(xpos, 1, kWave), est = __shfl_up(xst, 1, kWave);
-        if (l == 0) {
-            epos = entry_pos;
-            est = entry_st;
-        }
+        uint32_t epos = shift_up1(xpos, entry_pos), est = shift_up1(xst, entry_st);
         uint32_t fpos = 0, fst = 0;
-        for (int iter = 0; iter < kWave + 1; iter++) {
+        for (int iter = 0; iter <= kWave; iter++) {
             uint32_t pos = epos, st = est;
             bool merged = false, dead = false;
             while (pos < c1) {
@@ -378,50 +424,40 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                     dead = true;
                     break;
                 }
-                if (pos >= c0 && S.marks[pos - k.P] == st + 1) {
+                if (pos >= c0 && S.marks[pos - k.P] == ((st + 1) | (xgen << 2))) {
                     merged = true;
                     break;
                 }
                 const Step r = decode_one(S, k, pos, st);
                 if (r.bad || r.eof) {
-                    dead = true;                       // true-path EOF/errors seen in pass 3
+                    dead = true;                       // EOF / error: seen again in pass 3
                     break;
                 }
                 pos = r.pos;
                 st = r.st;
             }
-            if (merged) {
-                fpos = xpos;
-                fst = xst;
-            } else if (dead) {
-                fpos = kPosEnd;
-                fst = 0;
-            } else {
-                fpos = pos;
-                fst = st;
-            }
-            uint32_t npos = __shfl_up(fpos, 1, kWave), nst = __shfl_up(fst, 1, kWave);
-            if (l == 0) {
-                npos = entry_pos;
-                nst = entry_st;
-            }
+            fpos = merged ? xpos : (dead ? kPosEnd : pos);
+            fst = merged ? xst : (dead ? 0u : st);
+            const uint32_t npos = shift_up1(fpos, entry_pos), nst = shift_up1(fst, entry_st);
             const bool changed = npos != epos || nst != est;
+            if (STAMPS)
+                acc[PH_ITER] += 1;
             if (!wave_ballot(changed))
                 break;
             epos = npos;
             est = nst;
         }
-        // epos/est: true entry of this lane's segment (kPosEnd: none)
+        STAMP(PH_MERGE);
 
         // ---- pass 3: count ops of the true path ------------------------------
         uint32_t nops = 0;
-        bool lane_eof = false;
+        bool lane_eof = false, lane_err = false;
         {
             uint32_t pos = epos, st = est;
             while (pos < c1) {
                 const Step r = decode_one(S, k, pos, st);
                 if (r.bad) {
-                    k.err = true;
+                    lane_err = true;
                     break;
                 }
                 if (r.eof) {                           // EOF carries no op
@@ -429,7 +465,7 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                     break;
                 }
                 if (r.aL > kMaxOpLen || r.bL > kMaxOpLen) {
-                    k.err = true;
+                    lane_err = true;
                     break;
                 }
                 nops += (r.aL ? 1u : 0u) + (r.bL ? 1u : 0u);
@@ -437,12 +473,13 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                 st = r.st;
             }
         }
-        if (wave_ballot(k.err)) {
+        if (wave_ballot(lane_err)) {
             refuse = true;
             break;
         }
         const uint32_t incl = wave_incl_scan(nops);
         const uint32_t total_ops = lane_read(incl, kWave - 1);
+        STAMP(PH_COUNT);
         if (total_ops > kOpMax) {
             refuse = true;
             break;
@@ -470,19 +507,16 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
             }
         }
         wave_order();
-        const uint64_t eofm = wave_ballot(lane_eof);
-        // next piece's entry: exit of the last lane's true walk
-        {
-            const uint32_t lastp = lane_read(fpos, kWave - 1);
-            const uint32_t lasts = lane_read(fst, kWave - 1);
-            entry_pos = lastp;
-            entry_st = lasts;
-        }
-        if (eofm)
+        STAMP(PH_WRITE);
+        if (wave_ballot(lane_eof))
             done = true;
-        else if (entry_pos == kPosEnd) {               // dead without EOF
-            refuse = true;
-            break;
+        else {
+            entry_pos = lane_read(fpos, kWave - 1);     // next piece: the true exit
+            entry_st = lane_read(fst, kWave - 1);
+            if (entry_pos == kPosEnd) {                // dead without EOF
+                refuse = true;
+                break;
+            }
         }
 
         // ---- execute the piece's ops, 64 at a time ----------------------------
@@ -501,14 +535,13 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                 break;
             }
             const bool lit = (Sv & kLitFlag) != 0;
-            const uint32_t dist = Sv;
-            bool lb = l < nwin && !lit && dist > o;      // LOOKBEHIND_OVERRUN
+            const bool lb = l < nwin && !lit && Sv > o;     // LOOKBEHIND_OVERRUN
             if (wave_ballot(lb)) {
                 refuse = true;
                 break;
             }
             // end of each match's source range (periodic copies read only [o-d, o))
-            const uint32_t send = lit ? 0u : o - dist + (dist < L ? dist : L);
+            const uint32_t send = lit ? 0u : o - Sv + (Sv < L ? Sv : L);
             S.wo[l] = o;
             S.ws[l] = Sv;
             if (l == 0)
@@ -520,86 +553,77 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                 const bool brk = l > s && l < nwin && !lit && send > os;
                 const uint64_t bm = wave_ballot(brk);
                 const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nwin;
-                const uint32_t oe = e < (uint32_t)kWave ? S.wo[e] : carry + wtotal;
-                // ---- batch [s, e): output [os, oe) -------------------------
+                const uint32_t oe = e < nwin ? lane_read(o, e) : carry + wtotal;
+                STAMP(PH_FORM);
+                // ---- batch [s, e): output [os, oe), 64 dwords per step -------
                 const uint32_t base = os & ~3u;
-                const uint32_t units = (oe - base + 3) >> 2;
-                for (uint32_t u0 = 0; u0 < units; u0 += kWave) {
-                    // op of each lane's first byte: histogram of op starts + scan
-                    S.hist[l] = 0;
+                uint32_t jcarry = s;                    // first op starting at/after the step
+                for (uint32_t xs = base; xs < oe; xs += 4 * kWave) {
+                    // flag op starts per byte, count them per unit
+                    S.flags[l] = 0;
                     wave_order();
-                    if (l >= s && l < e) {
-                        const uint32_t c = (o - base + 3) >> 2;   // first unit starting at/after o
-                        const int32_t slot = (int32_t)c - (int32_t)u0;
-                        if (slot < kWave)
-                            atomicAdd(&S.hist[slot < 0 ? 0 : slot], 1u);
-                    }
+                    if (l >= s && l < e && o >= xs && o < xs + 4 * kWave)
+                        ((uint8_t*)S.flags)[o - xs] = 1;
                     wave_order();
-                    const uint32_t cnt = wave_incl_scan(S.hist[l]);
-                    const uint32_t u = u0 + l;
-                    if (u < units) {
-                        const uint32_t x = base + 4 * u;
-                        // op index j of byte x (s-1: belongs to an earlier batch)
-                        int32_t j = (int32_t)s + (int32_t)cnt - 1;
+                    const uint32_t f = S.flags[l];
+                    const uint32_t nst = (uint32_t)__builtin_popcount(f);
+                    const uint32_t sincl = wave_incl_scan(nst);
+                    const uint32_t jb = jcarry + sincl - nst - 1;   // op before this unit's starts
+                    jcarry += lane_read(sincl, kWave - 1);
+                    const uint32_t x = xs + 4 * l;
+                    if (x < oe) {
+                        const uint32_t step_end = xs + 4 * kWave;
+                        const uint32_t j0 = jb + (f & 1u);
                         uint32_t val = 0;
-                        const uint32_t step_end = base + 4 * (u0 + kWave);
-                        const uint32_t nxt_o = (j + 1 < (int32_t)e) ? S.wo[j + 1] : oe;
-                        bool fast = j >= (int32_t)s && x + 4 <= nxt_o && x + 4 <= oe;
-                        if (fast) {
-                            const uint32_t oj = S.wo[j];
-                            const uint32_t sj = S.ws[j];
+                        const bool single = (f >> 8) == 0 && x >= os && x + 4 <= oe;
+                        bool fast = false;
+                        if (single) {
+                            const uint32_t oj = S.wo[j0];
+                            const uint32_t sj = S.ws[j0];
                             const uint32_t r = x - oj;
                             if (sj & kLitFlag) {
                                 const uint32_t ip = (sj & ~kLitFlag) + r;
                                 const uint32_t rel = ip - k.P;
-                                if (rel + 4 <= k.staged) {
-                                    const uint32_t w0s = S.stage[rel >> 2];
-                                    const uint32_t w1s = S.stage[((rel >> 2) + 1) < kStageBytes / 4 ? (rel >> 2) + 1 : (rel >> 2)];
-                                    val = funnel(w0s, w1s, rel & 3u);
-                                } else
-                                    val = global_dword<false>(k.in + ip);
+                                val = rel + 4 <= k.staged ? stage_dword(S, rel)
+                                                          : global_dword<false>(k.in + ip);
+                                fast = true;
                             } else {
-                                const uint32_t d = sj;
-                                uint32_t rr = r;
-                                if (rr >= d)
-                                    rr %= d;
-                                if (rr + 4 <= d) {
-                                    const uint32_t y = oj - d + rr;
+                                const uint32_t Lj = S.wo[j0 + 1] - oj;
+                                const uint32_t y = match_src(oj, sj, Lj, r);
+                                if (y + 4 <= oj) {              // 4 contiguous source bytes
                                     if (y + kRing >= step_end + 4)
                                         val = ring_dword(S, y);
                                     else {
-                                        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): own stores landed
+                                        far_wait();
                                         val = global_dword<true>(k.out + y);
                                     }
-                                } else
-                                    fast = false;
+                                    fast = true;
+                                }
                             }
                         }
                         if (!fast) {
-                            // byte-serial assembly; ops may change inside the dword
-                            int32_t jj = j;
+                            val = 0;
+#pragma unroll
                             for (uint32_t q = 0; q < 4; q++) {
                                 const uint32_t xb = x + q;
-                                while (jj + 1 < (int32_t)e && S.wo[jj + 1] <= xb)
-                                    jj++;
+                                const uint32_t jq = jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u));
                                 uint32_t bv = 0;
-                                if (xb < os) {
-                                    bv = ring_byte(S, xb);            // earlier batch's byte
-                                } else if (xb < oe && jj >= (int32_t)s) {
-                                    const uint32_t oj = S.wo[jj];
-                                    const uint32_t sj = S.ws[jj];
+                                if (xb < os)
+                                    bv = ring_byte(S, xb);     // an earlier batch's byte
+                                else if (xb < oe) {
+                                    const uint32_t oj = S.wo[jq];
+                                    const uint32_t sj = S.ws[jq];
                                     const uint32_t r = xb - oj;
                                     if (sj & kLitFlag) {
                                         const uint32_t ip = (sj & ~kLitFlag) + r;
                                         const uint32_t rel = ip - k.P;
-                                        bv = rel < k.staged ? stage_byte(S, rel) : k.in[ip];
+                                        bv = rel < k.staged ? stage_byte(S, rel) : (uint32_t)k.in[ip];
                                     } else {
-                                        const uint32_t d = sj;
-                                        const uint32_t y = oj - d + (r >= d ? r % d : r);
+                                        const uint32_t y = match_src(oj, sj, S.wo[jq + 1] - oj, r);
                                         if (y + kRing >= step_end + 4)
                                             bv = ring_byte(S, y);
                                         else {
-                                            __builtin_amdgcn_s_waitcnt(0x0F70);
+                                            far_wait();
                                             bv = global_byte_nt(k.out + y);
                                         }
                                     }
@@ -613,10 +637,11 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                         if (x + 4 <= oe)
                             *(uint32_t*)(k.out + x) = val;
                         else
-                            for (uint32_t q = 0; q < 4 && x + q < oe; q++)
+                            for (uint32_t q = 0; x + q < oe; q++)
                                 k.out[x + q] = (uint8_t)(val >> (8 * q));
                     }
                     wave_order();
+                    STAMP(PH_STEPS);
                 }
                 s = e;
             }
@@ -626,6 +651,10 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
         k.P += kPiece;
     }
 
+    if (STAMPS && l == 0)
+        for (int i = 0; i < 8; i++)
+            stamps[(size_t)b * 8 + i] = acc[i];
+#undef STAMP
     if (l == 0) {
         if (refuse) {
             status[b] = kFallback;
@@ -649,8 +678,22 @@ extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint6
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_decode_fast_kernel, dim3(nblocks), dim3(kWave), 0, stream, src,
-                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
-                       nblocks);
+    hipLaunchKernelGGL(lzo1x_decode_fast_kernel<false>, dim3(nblocks), dim3(kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
+                       nblocks, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Diagnostic: the same decoder with per-phase cycle stamps (8 x u64 per block).
+extern "C" int lzo_mi355x_debug_decompress_fast_stamps(
+    const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint8_t* dst,
+    const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* out_len, int32_t* status,
+    uint32_t* fallback, uint32_t nblocks, uint64_t* stamps, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_decode_fast_kernel<true>, dim3(nblocks), dim3(kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
+                       nblocks, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

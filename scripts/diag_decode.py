@@ -1,0 +1,57 @@
+"""Diagnostic: phase breakdown of the fast decoder (s_memtime stamps build).
+Usage: python scripts/diag_decode.py [--blocks N] [--model itb]"""
+import argparse, ctypes, os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch
+from pomegranate_amd import lzo, synth
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--blocks", type=int, default=4096)
+ap.add_argument("--model", default="itb")
+ap.add_argument("--bytes", type=int, default=65536)
+a = ap.parse_args()
+dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
+lib = lzo.load()
+model = {v: k for k, v in synth.MODEL_NAMES.items()}[a.model]
+arena, offs, lens = synth.batch(model, 0, [a.bytes] * a.blocks, threads=16)
+t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+nb = a.blocks
+src = lzo.DeviceBatch(t(arena), t(offs.view(np.int64)), t(lens.view(np.int32)))
+caps = np.array([lzo.worst_compress(int(n)) for n in lens], dtype=np.uint32)
+zo = np.zeros(nb, dtype=np.uint64); zo[1:] = np.cumsum((caps[:-1].astype(np.uint64) + 255) // 256 * 256)
+za = torch.zeros(int(zo[-1]) + int(caps[-1]) + 256, dtype=torch.uint8, device=dev)
+zb = lzo.DeviceBatch(za, t(zo.view(np.int64)), t(caps.view(np.int32)))
+zl = torch.zeros(nb, dtype=torch.int32, device=dev); zs = torch.zeros_like(zl)
+lzo.compress_dev(src, zb, zl, zs); torch.cuda.synchronize()
+zsrc = lzo.DeviceBatch(za, zb.off, zl)
+out = torch.zeros_like(src.arena); ob = lzo.DeviceBatch(out, src.off, src.length)
+ol = torch.zeros_like(zl); os_ = torch.zeros_like(zl)
+fb = torch.zeros(nb + 1, dtype=torch.int32, device=dev)
+stamps = torch.zeros(nb * 8, dtype=torch.int64, device=dev)
+fn = lib.lzo_mi355x_debug_decompress_fast_stamps
+fn.restype = ctypes.c_int
+fn.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+fast = lib.lzo_mi355x_launch_decompress_fast
+fast.restype = ctypes.c_int
+fast.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_uint32, ctypes.c_void_p]
+p = lambda x: x.data_ptr()
+sh = torch.cuda.current_stream().cuda_stream
+def run(stamp):
+    fb.zero_()
+    if stamp:
+        fn(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), nb, p(stamps), sh)
+    else:
+        fast(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), nb, sh)
+for stamp in (False, True):
+    run(stamp); torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(); run(stamp); e1.record(); torch.cuda.synchronize()
+    print(f"stamps={stamp}: kernel {e0.elapsed_time(e1):.3f} ms, fallback {int(fb[0].item())}, "
+          f"equal {torch.equal(out, src.arena)}")
+st = stamps.view(nb, 8).double().cpu().numpy()
+names = ["stage", "pass1", "merge", "count", "write", "form", "steps", "merge_iters"]
+tot = st.sum(1)
+print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(names)}, "total", int(tot.mean()))
+print("zlen mean", float(zl.double().mean()))
