@@ -45,7 +45,8 @@ constexpr uint32_t kLook = 24;                   // speculative lead-in before a
 constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
 constexpr uint32_t kOpMax = 512;                 // ops per piece
-constexpr uint32_t kRing = 8192;                 // recent output kept in LDS
+constexpr uint32_t kRing = 16384;                // recent output kept in LDS
+constexpr uint32_t kRingSlack = 1024;            // decoder keeps this much ring unflushed-free
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kLitFlag = 0x80000000u;
 constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wrap 32 bits
@@ -67,6 +68,10 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t ws[kWave + 4];
     uint32_t flags[kWave];
     uint8_t marks[kPiece];
+    // decoder -> writer hand-off (LDS words, workgroup scope)
+    uint32_t produced;      // output bytes final in the ring
+    uint32_t flushed;       // output bytes stored to HBM and landed
+    uint32_t state;         // 0 running, 1 finished, 2 refused
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -94,6 +99,15 @@ __device__ __forceinline__ uint32_t shift_up1(uint32_t v, uint32_t fill)
     return lane_id() == 0 ? fill : u;
 }
 
+__device__ __forceinline__ uint32_t lds_load(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 struct Blk {
     const uint8_t* in;      // compressed block
     uint32_t z;             // its length
@@ -116,7 +130,7 @@ __device__ __forceinline__ uint32_t rdin(const FastLds& s, const Blk& k, uint32_
     const uint32_t r = pos - k.P;
     if (r < k.staged)
         return stage_byte(s, r);
-    return k.in[pos];
+    return *((__attribute__((address_space(1))) const uint8_t*)(k.in + pos));
 }
 
 // One instruction from (pos, st).  Produces up to two ops (A: literal run or
@@ -266,11 +280,18 @@ __device__ __forceinline__ uint32_t stage_dword(const FastLds& s, uint32_t r)
 // 4 bytes at an arbitrary global address via two aligned dword loads (an
 // aligned dword that overlaps valid bytes never leaves their page).  NT: L2
 // served (the vector L1 is not coherent with this wave's earlier stores).
+typedef __attribute__((address_space(1))) const uint32_t gdword;
+
+// 4 bytes at an arbitrary global address via two aligned dword loads (an
+// aligned dword that overlaps valid bytes never leaves their page).  NT: L2
+// served (the vector L1 is not coherent with the writer wave's stores).
+// Address-space-1 pointers keep these global_load (vmcnt only), not flat_load
+// (which also waits on lgkmcnt and so on every outstanding LDS access).
 template <bool NT>
 __device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
 {
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    gdword* q = (gdword*)(a & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(a & 3);
     uint32_t w0, w1 = 0;
     if (NT) {
@@ -288,15 +309,9 @@ __device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
 __device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
 {
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t w = __builtin_nontemporal_load((const uint32_t*)(a & ~(uintptr_t)3));
+    const uint32_t w = __builtin_nontemporal_load((gdword*)(a & ~(uintptr_t)3));
     return (w >> (8u * (uint32_t)(a & 3))) & 0xFFu;
 }
-
-// A far match source y (beyond the ring) was stored >= (kRing-256)/256 = 31
-// steps ago, one or more global stores per step: once at most 16 of this
-// wave's vector-memory operations are outstanding, that store has landed in
-// L2 (vmcnt retires in issue order), and the L2-served load below sees it.
-__device__ __forceinline__ void far_wait() { __builtin_amdgcn_s_waitcnt(0x4F70); }   // vmcnt(16)
 
 __device__ __forceinline__ uint32_t match_src(uint32_t oj, uint32_t d, uint32_t L, uint32_t r)
 {
@@ -307,11 +322,93 @@ __device__ __forceinline__ uint32_t match_src(uint32_t oj, uint32_t d, uint32_t 
 
 // Diagnostic build only (STAMPS): per-phase s_memtime cycle sums go to
 // stamps[b * 8 + phase]; no output value depends on them.
-enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_ITER };
+enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_WALKS };
+
+// Uniform walk of the true path from (pos, st) through lane i's segment
+// [c0, c1) until it lands on one of lane i's final-generation marks (then
+// lane i's speculative exit is the answer) or leaves the segment.
+__device__ __forceinline__ void walk_uniform(const FastLds& S, const Blk& k, uint32_t c0,
+                                             uint32_t c1, uint32_t gen, uint32_t xpos,
+                                             uint32_t xst, uint32_t& pos, uint32_t& st)
+{
+    while (pos < c1) {
+        if (pos >= k.z) {
+            pos = kPosEnd;
+            st = 0;
+            return;
+        }
+        if (pos >= c0 && S.marks[pos - k.P] == ((st + 1) | (gen << 2))) {
+            pos = xpos;
+            st = xst;
+            return;
+        }
+        const Step r = decode_one(S, k, pos, st);
+        if (r.bad || r.eof) {
+            pos = kPosEnd;
+            st = 0;
+            return;
+        }
+        pos = r.pos;
+        st = r.st;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Writer wave: copies final output from the LDS ring to HBM with 16-byte
+// stores, keeping a few chunks in flight; publishes `flushed` once stores have
+// landed.  It issues no loads, so its stores never hold up the decoder wave's
+// loads (gfx9 vmcnt retires loads and stores in one in-order queue per wave).
+// ---------------------------------------------------------------------------
+__device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
+{
+    constexpr uint32_t kChunk = 16 * kWave;        // 1 KiB per store instruction
+    uint32_t issued = 0;
+    uint32_t pend[4] = {0, 0, 0, 0};               // ends of chunks in flight, oldest first
+    uint32_t npend = 0;
+    for (;;) {
+        const uint32_t state = lds_load(&S.state);
+        const uint32_t prod = lds_load(&S.produced);
+        if (state == 2)
+            return;                                // refused: exact decoder redoes the block
+        const uint32_t upto = state == 1 ? prod : (prod & ~15u);
+        if (upto > issued && (upto - issued >= kChunk || state == 1)) {
+            const uint32_t end = upto - issued > kChunk ? issued + kChunk : upto;
+            const uint32_t x = issued + 16 * l;
+            if (x + 16 <= end) {
+                const uint32_t i = x & kRingMask;
+                const uint4 v = *(const uint4*)&S.ring[i >> 2];
+                *(uint4*)(out + x) = v;
+            } else if (x < end) {
+                for (uint32_t q = 0; x + q < end; q++)
+                    out[x + q] = (uint8_t)ring_byte(S, x + q);
+            }
+            issued = end;
+            if (npend == 4) {
+                __builtin_amdgcn_s_waitcnt(0x0F73);        // vmcnt(3): oldest chunk landed
+                lds_store(&S.flushed, pend[0]);
+                pend[0] = pend[1];
+                pend[1] = pend[2];
+                pend[2] = pend[3];
+                npend = 3;
+            }
+            pend[npend++] = end;
+            continue;
+        }
+        if (npend) {                               // nothing new: drain and publish
+            __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
+            lds_store(&S.flushed, issued);
+            npend = 0;
+            continue;
+        }
+        if (state == 1)
+            return;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
 
 // ---------------------------------------------------------------------------
 template <bool STAMPS>
-__global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
+__global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
@@ -319,6 +416,24 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
     uint32_t* __restrict__ fallback, uint32_t nblocks, uint64_t* __restrict__ stamps)
 {
     __shared__ FastLds S;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t l = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x == 0) {
+        S.produced = 0;
+        S.flushed = 0;
+        S.state = 0;
+    }
+    __syncthreads();
+    uint8_t* const out = dst + dst_off[b];
+    if (wave == 1) {
+        // The decoder refuses misaligned destinations before publishing anything.
+        writer_wave(S, out, l);
+        return;
+    }
+
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(ph)                                                   \
@@ -330,23 +445,20 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
         }                                                           \
     } while (0)
 
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks)
-        return;
-    const uint32_t l = lane_id();
     Blk k;
     k.in = src + src_off[b];
     k.z = src_len[b];
-    k.out = dst + dst_off[b];
+    k.out = out;
     k.cap = dst_cap[b];
     k.P = 0;
     k.staged = 0;
 
-    // The exact decoder takes: misaligned destinations, empty or huge blocks
-    // (lengths up to 255 * z must not wrap 32 bits).
-    bool refuse = ((uintptr_t)k.out & 3) != 0 || k.z >= (1u << 24) || k.z == 0;
+    // The exact decoder takes: destinations not 16-byte aligned, empty or huge
+    // blocks (lengths up to 255 * z must not wrap 32 bits).
+    bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
     uint32_t entry_pos = 0, entry_st = ST_F;   // true entry of the current piece
     uint32_t carry = 0;                        // output produced so far
+    uint32_t flushed_seen = 0;                 // last `flushed` read
     bool done = false;                         // EOF consumed
 
     while (!refuse && !done) {
@@ -413,40 +525,36 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
         wave_order();
         STAMP(PH_PASS1);
 
-        // ---- resolve true entries: walk until merged into own marks ----------
-        uint32_t epos = shift_up1(xpos, entry_pos), est = shift_up1(xst, entry_st);
-        uint32_t fpos = 0, fst = 0;
-        for (int iter = 0; iter <= kWave; iter++) {
-            uint32_t pos = epos, st = est;
-            bool merged = false, dead = false;
-            while (pos < c1) {
-                if (pos >= k.z) {
-                    dead = true;
-                    break;
+        // ---- true entries: one parallel walk from the assumed entries, then a
+        // scalar scan that reuses it and walks only where the guess was wrong.
+        const uint32_t apos = shift_up1(xpos, entry_pos), ast = shift_up1(xst, entry_st);
+        uint32_t fpos = apos, fst = ast;
+        walk_uniform(S, k, c0, c1, xgen, xpos, xst, fpos, fst);   // per lane (divergent)
+        uint32_t epos = 0, est = 0;
+        {
+            uint32_t E = entry_pos, Est = entry_st;
+            for (uint32_t i = 0; i < (uint32_t)kWave; i++) {
+                if (l == i) {
+                    epos = E;
+                    est = Est;
                 }
-                if (pos >= c0 && S.marks[pos - k.P] == ((st + 1) | (xgen << 2))) {
-                    merged = true;
-                    break;
+                const uint32_t ci1 = k.P + (i + 1) * kSeg;
+                if (E >= ci1)
+                    continue;                          // segment i has no true start
+                if (E == lane_read(apos, i) && Est == lane_read(ast, i)) {
+                    E = lane_read(fpos, i);
+                    Est = lane_read(fst, i);
+                    continue;
                 }
-                const Step r = decode_one(S, k, pos, st);
-                if (r.bad || r.eof) {
-                    dead = true;                       // EOF / error: seen again in pass 3
-                    break;
-                }
-                pos = r.pos;
-                st = r.st;
+                walk_uniform(S, k, ci1 - kSeg, ci1, lane_read(xgen, i), lane_read(xpos, i),
+                             lane_read(xst, i), E, Est);
+                if (STAMPS)
+                    acc[PH_WALKS] += 1;
             }
-            fpos = merged ? xpos : (dead ? kPosEnd : pos);
-            fst = merged ? xst : (dead ? 0u : st);
-            const uint32_t npos = shift_up1(fpos, entry_pos), nst = shift_up1(fst, entry_st);
-            const bool changed = npos != epos || nst != est;
-            if (STAMPS)
-                acc[PH_ITER] += 1;
-            if (!wave_ballot(changed))
-                break;
-            epos = npos;
-            est = nst;
+            fpos = E;                                  // (only lane 63's value is used)
+            fst = Est;
         }
+        const uint32_t next_pos = fpos, next_st = fst;
         STAMP(PH_MERGE);
 
         // ---- pass 3: count ops of the true path ------------------------------
@@ -511,8 +619,8 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
         if (wave_ballot(lane_eof))
             done = true;
         else {
-            entry_pos = lane_read(fpos, kWave - 1);     // next piece: the true exit
-            entry_st = lane_read(fst, kWave - 1);
+            entry_pos = next_pos;                      // next piece: the true exit
+            entry_st = next_st;
             if (entry_pos == kPosEnd) {                // dead without EOF
                 refuse = true;
                 break;
@@ -559,10 +667,18 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                 const uint32_t base = os & ~3u;
                 uint32_t jcarry = s;                    // first op starting at/after the step
                 for (uint32_t xs = base; xs < oe; xs += 4 * kWave) {
+                    const uint32_t step_end = xs + 4 * kWave;
+                    // ring space: positions [step_end - kRing, xs) must be flushed
+                    // before this step overwrites their slots (and far reads
+                    // below need flushed >= step_end - kRing + kRingSlack).
+                    while (step_end > flushed_seen + kRing - kRingSlack) {
+                        __builtin_amdgcn_s_sleep(1);
+                        flushed_seen = lds_load(&S.flushed);
+                    }
                     // flag op starts per byte, count them per unit
                     S.flags[l] = 0;
                     wave_order();
-                    if (l >= s && l < e && o >= xs && o < xs + 4 * kWave)
+                    if (l >= s && l < e && o >= xs && o < step_end)
                         ((uint8_t*)S.flags)[o - xs] = 1;
                     wave_order();
                     const uint32_t f = S.flags[l];
@@ -572,7 +688,6 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                     jcarry += lane_read(sincl, kWave - 1);
                     const uint32_t x = xs + 4 * l;
                     if (x < oe) {
-                        const uint32_t step_end = xs + 4 * kWave;
                         const uint32_t j0 = jb + (f & 1u);
                         uint32_t val = 0;
                         const bool single = (f >> 8) == 0 && x >= os && x + 4 <= oe;
@@ -591,12 +706,8 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                                 const uint32_t Lj = S.wo[j0 + 1] - oj;
                                 const uint32_t y = match_src(oj, sj, Lj, r);
                                 if (y + 4 <= oj) {              // 4 contiguous source bytes
-                                    if (y + kRing >= step_end + 4)
-                                        val = ring_dword(S, y);
-                                    else {
-                                        far_wait();
-                                        val = global_dword<true>(k.out + y);
-                                    }
+                                    val = y + kRing >= step_end + 4 ? ring_dword(S, y)
+                                                                    : global_dword<true>(k.out + y);
                                     fast = true;
                                 }
                             }
@@ -617,32 +728,24 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
                                     if (sj & kLitFlag) {
                                         const uint32_t ip = (sj & ~kLitFlag) + r;
                                         const uint32_t rel = ip - k.P;
-                                        bv = rel < k.staged ? stage_byte(S, rel) : (uint32_t)k.in[ip];
+                                        bv = rel < k.staged ? stage_byte(S, rel)
+                                                            : (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + ip));
                                     } else {
                                         const uint32_t y = match_src(oj, sj, S.wo[jq + 1] - oj, r);
-                                        if (y + kRing >= step_end + 4)
-                                            bv = ring_byte(S, y);
-                                        else {
-                                            far_wait();
-                                            bv = global_byte_nt(k.out + y);
-                                        }
+                                        bv = y + kRing >= step_end + 4 ? ring_byte(S, y)
+                                                                       : global_byte_nt(k.out + y);
                                     }
                                 }
                                 val |= bv << (8 * q);
                             }
                         }
                         S.ring[(x & kRingMask) >> 2] = val;
-                        // Bytes past oe are not known yet: the next batch's first
-                        // unit stores the whole dword.  Nothing past oe (<= cap).
-                        if (x + 4 <= oe)
-                            *(uint32_t*)(k.out + x) = val;
-                        else
-                            for (uint32_t q = 0; x + q < oe; q++)
-                                k.out[x + q] = (uint8_t)(val >> (8 * q));
                     }
                     wave_order();
                     STAMP(PH_STEPS);
                 }
+                // bytes below oe are final: hand them to the writer wave
+                lds_store(&S.produced, oe);
                 s = e;
             }
             carry += wtotal;
@@ -657,10 +760,13 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_fast_kernel(
 #undef STAMP
     if (l == 0) {
         if (refuse) {
+            lds_store(&S.state, 2u);
             status[b] = kFallback;
             const uint32_t at = atomicAdd(&fallback[0], 1u);
             fallback[1 + at] = b;
         } else {
+            lds_store(&S.produced, carry);
+            lds_store(&S.state, 1u);
             out_len[b] = carry;
             status[b] = 0;
         }
@@ -678,9 +784,9 @@ extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint6
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_decode_fast_kernel<false>, dim3(nblocks), dim3(kWave), 0, stream,
-                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
-                       nblocks, nullptr);
+    hipLaunchKernelGGL(lzo1x_decode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0,
+                       stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
+                       fallback, nblocks, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -692,8 +798,8 @@ extern "C" int lzo_mi355x_debug_decompress_fast_stamps(
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_decode_fast_kernel<true>, dim3(nblocks), dim3(kWave), 0, stream,
-                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
-                       nblocks, stamps);
+    hipLaunchKernelGGL(lzo1x_decode_fast_kernel<true>, dim3(nblocks), dim3(2 * kWave), 0,
+                       stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
+                       fallback, nblocks, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

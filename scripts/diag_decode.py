@@ -51,7 +51,7 @@ for stamp in (False, True):
     print(f"stamps={stamp}: kernel {e0.elapsed_time(e1):.3f} ms, fallback {int(fb[0].item())}, "
           f"equal {torch.equal(out, src.arena)}")
 st = stamps.view(nb, 8).double().cpu().numpy()
-names = ["stage", "pass1", "merge", "count", "write", "form", "steps", "merge_iters"]
+names = ["stage", "pass1", "merge", "count", "write", "form", "steps", "walks"]
 tot = st.sum(1)
 print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(names)}, "total", int(tot.mean()))
 print("zlen mean", float(zl.double().mean()))
