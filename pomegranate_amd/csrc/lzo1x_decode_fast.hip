@@ -365,7 +365,7 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
     uint32_t issued = 0;
     uint32_t pend[4] = {0, 0, 0, 0};               // ends of chunks in flight, oldest first
     uint32_t npend = 0;
-    for (;;) {
+    for (uint32_t spin = 0; spin < (1u << 24); spin++) {
         const uint32_t state = lds_load(&S.state);
         const uint32_t prod = lds_load(&S.produced);
         if (state == 2)
@@ -671,10 +671,16 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                     // ring space: positions [step_end - kRing, xs) must be flushed
                     // before this step overwrites their slots (and far reads
                     // below need flushed >= step_end - kRing + kRingSlack).
-                    while (step_end > flushed_seen + kRing - kRingSlack) {
+                    for (uint32_t spin = 0; step_end > flushed_seen + kRing - kRingSlack; spin++) {
+                        if (spin > (1u << 22)) {       // writer stuck: let the exact path redo it
+                            refuse = true;
+                            break;
+                        }
                         __builtin_amdgcn_s_sleep(1);
                         flushed_seen = lds_load(&S.flushed);
                     }
+                    if (refuse)
+                        break;
                     // flag op starts per byte, count them per unit
                     S.flags[l] = 0;
                     wave_order();
@@ -742,10 +748,12 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                         S.ring[(x & kRingMask) >> 2] = val;
                     }
                     wave_order();
+                    // bytes below min(step_end, oe) are final: hand them over
+                    lds_store(&S.produced, step_end < oe ? step_end : oe);
                     STAMP(PH_STEPS);
                 }
-                // bytes below oe are final: hand them to the writer wave
-                lds_store(&S.produced, oe);
+                if (refuse)
+                    break;
                 s = e;
             }
             carry += wtotal;

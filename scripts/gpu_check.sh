@@ -17,6 +17,6 @@ step() {  # step NAME SECONDS CMD...
     return 0
 }
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo build failed; tail gpurun_out/build.log; exit 1; }
-step pytest_gpu 900 python -m pytest tests -q -m gpu -x
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 400 python bench.py "$@"
+step pytest_gpu 360 python -m pytest tests -q -m gpu -x
+step smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 360 python bench.py "$@"
