@@ -33,6 +33,7 @@
 // destination...) marks the block for the exact decoder (lzo1x_kernels.hip),
 // which produces the reference's output and LZO_E_* code bit for bit.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "lzo_mi355x_kernels.h"
@@ -66,6 +67,7 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t opS[kOpMax];
     uint32_t wo[kWave + 4];
     uint32_t ws[kWave + 4];
+    uint32_t wm[kWave + 4];   // periodic-match reciprocal: ceil(2^32 / d), 0 = not periodic
     uint32_t flags[kWave];
     uint8_t marks[kPiece];
     // decoder -> writer hand-off (LDS words, workgroup scope)
@@ -73,6 +75,11 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t flushed;       // output bytes stored to HBM and landed
     uint32_t state;         // 0 running, 1 finished, 2 refused
 };
+
+constexpr uint32_t kRingOff = 0;                                  // offsetof(FastLds, ring)
+constexpr uint32_t kStageOff = kRing;                             // offsetof(FastLds, stage)
+static_assert(offsetof(FastLds, ring) == kRingOff, "layout");
+static_assert(offsetof(FastLds, stage) == kStageOff, "layout");
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
@@ -161,7 +168,7 @@ __device__ __forceinline__ uint32_t read_ext(const FastLds& s, const Blk& k, uin
     return v;
 }
 
-__device__ __forceinline__ Step decode_one(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st)
+__device__ __noinline__ Step decode_one(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st)
 {
     Step r;
     r.aL = r.bL = 0;
@@ -250,6 +257,87 @@ __device__ __forceinline__ Step decode_one(const FastLds& s, const Blk& k, uint3
     return r;
 }
 
+// Branch-free form of decode_one for the common case: the instruction lies in
+// the staged input and any length extension is a single non-zero byte.  One
+// LDS round trip (three aligned dwords -> 8 bytes at pos), then selects; lanes
+// decoding different instruction kinds do not diverge.  Falls back to
+// decode_one otherwise (long extensions, input beyond the staging window).
+__device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st)
+{
+    const uint32_t rel = pos - k.P;
+    if (rel + 12 > kStageBytes || pos >= k.z)
+        return decode_one(s, k, pos, st);
+    const uint32_t w0 = s.stage[rel >> 2], w1 = s.stage[(rel >> 2) + 1], w2 = s.stage[(rel >> 2) + 2];
+    const uint32_t sh = 8u * (rel & 3u);
+    const uint64_t lo64 = ((uint64_t)w1 << 32) | w0;
+    const uint32_t lo = (uint32_t)(lo64 >> sh);
+    const uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
+    const uint64_t b8 = ((uint64_t)hi << 32) | lo;                 // bytes pos..pos+7
+#define BYTE(i) ((uint32_t)(b8 >> (8u * (i))) & 0xFFu)
+    const uint32_t t = lo & 0xFFu, b1 = BYTE(1);
+    Step r;
+    r.eof = false;
+    r.bL = r.bS = 0;
+    const bool first = st == ST_F;
+    if (first && t > 17) {                                         // :3357-3365
+        const uint32_t n = t - 17;
+        r.aL = n;
+        r.aS = kLitFlag | (pos + 1);
+        r.pos = pos + 1 + n;
+        r.st = n < 4 ? ST_C : ST_B;
+        r.bad = r.pos > k.z;
+        return r;
+    }
+    const uint32_t se = first ? ST_A : st;
+    // extension byte needed: literal run t == 0, M3 with t&31 == 0, M4 with t&7 == 0
+    const bool lit = se == ST_A && t < 16;
+    const bool ext = (lit && t == 0) || (t >= 32 && t < 64 && (t & 31) == 0) ||
+                     (t >= 16 && t < 32 && (t & 7) == 0);
+    if (ext && b1 == 0)
+        return decode_one(s, k, pos, st);                          // 255-chunk extension
+    const uint32_t e = ext ? 1u : 0u;
+    if (lit) {                                                     // :3367-3414
+        const uint32_t n = (ext ? 15u + b1 : t) + 3u;
+        r.aL = n;
+        r.aS = kLitFlag | (pos + 1 + e);
+        r.pos = pos + 1 + e + n;
+        r.st = ST_B;
+        r.bad = r.pos > k.z;
+        return r;
+    }
+    // matches: M1 (t < 16), M2 (t >= 64), M3 (32..63), M4 (16..31)
+    const uint32_t o16 = BYTE(1 + e) | (BYTE(2 + e) << 8);
+    const uint32_t dm1 = (se == ST_B ? 0x801u : 1u) + (t >> 2) + (b1 << 2);
+    const uint32_t dm2 = 1u + ((t >> 2) & 7u) + (b1 << 3);
+    const uint32_t dm3 = 1u + (o16 >> 2);
+    const uint32_t dd4 = ((t & 8u) << 11) + (o16 >> 2);
+    const bool m1 = t < 16, m2 = t >= 64, m3 = t >= 32 && t < 64;
+    const uint32_t L = m1 ? (se == ST_B ? 3u : 2u)
+                     : m2 ? (t >> 5) + 1u
+                     : m3 ? (ext ? 31u + b1 : (t & 31u)) + 2u
+                          : (ext ? 7u + b1 : (t & 7u)) + 2u;
+    const uint32_t d = m1 ? dm1 : m2 ? dm2 : m3 ? dm3 : dd4 + 0x4000u;
+    const uint32_t used = (m1 || m2) ? 2u : 3u + e;
+    if (!m1 && !m2 && !m3 && dd4 == 0) {                           // EOF, :3580
+        r.eof = true;
+        r.pos = pos + used;
+        r.st = ST_A;
+        r.aL = r.aS = 0;
+        r.bad = r.pos != k.z;
+        return r;
+    }
+    const uint32_t tl = BYTE(used - 2) & 3u;                       // match_done, :3650
+#undef BYTE
+    r.aL = L;
+    r.aS = d;
+    r.bL = tl;
+    r.bS = kLitFlag | (pos + used);
+    r.pos = pos + used + tl;
+    r.st = tl ? ST_C : ST_A;
+    r.bad = r.pos > k.z;
+    return r;
+}
+
 // Output / input byte helpers -------------------------------------------------
 __device__ __forceinline__ uint32_t ring_byte(const FastLds& s, uint32_t y)
 {
@@ -262,20 +350,7 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
 }
 
-__device__ __forceinline__ uint32_t ring_dword(const FastLds& s, uint32_t y)
-{
-    const uint32_t i = y & kRingMask;
-    const uint32_t w0 = s.ring[i >> 2];
-    const uint32_t w1 = s.ring[((i >> 2) + 1) & (kRingMask >> 2)];
-    return funnel(w0, w1, i & 3u);
-}
 
-__device__ __forceinline__ uint32_t stage_dword(const FastLds& s, uint32_t r)
-{
-    const uint32_t w0 = s.stage[r >> 2];
-    const uint32_t w1 = (r & 3u) ? s.stage[(r >> 2) + 1] : 0u;
-    return funnel(w0, w1, r & 3u);
-}
 
 // 4 bytes at an arbitrary global address via two aligned dword loads (an
 // aligned dword that overlaps valid bytes never leaves their page).  NT: L2
@@ -313,16 +388,11 @@ __device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
     return (w >> (8u * (uint32_t)(a & 3))) & 0xFFu;
 }
 
-__device__ __forceinline__ uint32_t match_src(uint32_t oj, uint32_t d, uint32_t L, uint32_t r)
-{
-    // byte-serial overlap semantics: out[o + r] = out[o - d + (r mod d)]
-    const uint32_t rr = (d < L && r >= d) ? r % d : r;
-    return oj - d + rr;
-}
 
 // Diagnostic build only (STAMPS): per-phase s_memtime cycle sums go to
 // stamps[b * 8 + phase]; no output value depends on them.
-enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_WALKS };
+enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_WALKS,
+       PH_SPACE, PH_FLAGS, PH_GATHER, PH_NSTEP, PH_NBATCH, PH_NSLOW, PH_N };
 
 // Uniform walk of the true path from (pos, st) through lane i's segment
 // [c0, c1) until it lands on one of lane i's final-generation marks (then
@@ -342,7 +412,7 @@ __device__ __forceinline__ void walk_uniform(const FastLds& S, const Blk& k, uin
             st = xst;
             return;
         }
-        const Step r = decode_one(S, k, pos, st);
+        const Step r = decode_step(S, k, pos, st);
         if (r.bad || r.eof) {
             pos = kPosEnd;
             st = 0;
@@ -434,7 +504,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
         return;
     }
 
-    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t acc[PH_N] = {};
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(ph)                                                   \
     do {                                                            \
@@ -508,7 +578,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
             while (pos < c1 && pos < k.z) {
                 if (pos >= c0)
                     S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 2));
-                const Step r = decode_one(S, k, pos, st);
+                const Step r = decode_step(S, k, pos, st);
                 if (r.bad || r.eof) {                  // impossible guess: restart later
                     pos++;
                     st = ST_A;
@@ -563,7 +633,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
         {
             uint32_t pos = epos, st = est;
             while (pos < c1) {
-                const Step r = decode_one(S, k, pos, st);
+                const Step r = decode_step(S, k, pos, st);
                 if (r.bad) {
                     lane_err = true;
                     break;
@@ -597,7 +667,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
             uint32_t w = incl - nops;
             uint32_t pos = epos, st = est;
             while (pos < c1) {
-                const Step r = decode_one(S, k, pos, st);
+                const Step r = decode_step(S, k, pos, st);
                 if (r.eof)
                     break;
                 if (r.aL) {
@@ -650,8 +720,15 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
             }
             // end of each match's source range (periodic copies read only [o-d, o))
             const uint32_t send = lit ? 0u : o - Sv + (Sv < L ? Sv : L);
+            // A periodic match (d < L) repeats its first d bytes: for any byte x
+            // and any W <= x with W >= o, out[x] = out[x - d*m], m = (x-W)/d + 1
+            // (the source then lies in [W - d, W), already written).  Within one
+            // 256-byte step x - W <= 258, so only d <= 258 needs the division,
+            // done as a multiply-high by ceil(2^32/d) (exact for these sizes).
+            const bool per = !lit && Sv < L && Sv <= 258;
             S.wo[l] = o;
             S.ws[l] = Sv;
+            S.wm[l] = !per ? 0u : Sv == 1 ? 0xFFFFFFFFu : (uint32_t)(0xFFFFFFFFu / Sv) + 1u;
             if (l == 0)
                 S.wo[kWave] = carry + wtotal;
             wave_order();
@@ -663,6 +740,8 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                 const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nwin;
                 const uint32_t oe = e < nwin ? lane_read(o, e) : carry + wtotal;
                 STAMP(PH_FORM);
+                if (STAMPS)
+                    acc[PH_NBATCH] += 1;
                 // ---- batch [s, e): output [os, oe), 64 dwords per step -------
                 const uint32_t base = os & ~3u;
                 uint32_t jcarry = s;                    // first op starting at/after the step
@@ -681,6 +760,9 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                     }
                     if (refuse)
                         break;
+                    STAMP(PH_SPACE);
+                    if (STAMPS)
+                        acc[PH_NSTEP] += 1;
                     // flag op starts per byte, count them per unit
                     S.flags[l] = 0;
                     wave_order();
@@ -692,62 +774,63 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                     const uint32_t sincl = wave_incl_scan(nst);
                     const uint32_t jb = jcarry + sincl - nst - 1;   // op before this unit's starts
                     jcarry += lane_read(sincl, kWave - 1);
+                    STAMP(PH_FLAGS);
                     const uint32_t x = xs + 4 * l;
                     if (x < oe) {
-                        const uint32_t j0 = jb + (f & 1u);
+                        // Every byte the same way (no divergent paths): its op's
+                        // affine source -> one LDS byte read (stage or ring).
+                        const uint32_t W = os > xs ? os : xs;   // bytes below W are written
+                        const uint8_t* lds = (const uint8_t*)&S;
                         uint32_t val = 0;
-                        const bool single = (f >> 8) == 0 && x >= os && x + 4 <= oe;
-                        bool fast = false;
-                        if (single) {
-                            const uint32_t oj = S.wo[j0];
-                            const uint32_t sj = S.ws[j0];
-                            const uint32_t r = x - oj;
-                            if (sj & kLitFlag) {
-                                const uint32_t ip = (sj & ~kLitFlag) + r;
-                                const uint32_t rel = ip - k.P;
-                                val = rel + 4 <= k.staged ? stage_dword(S, rel)
-                                                          : global_dword<false>(k.in + ip);
-                                fast = true;
-                            } else {
-                                const uint32_t Lj = S.wo[j0 + 1] - oj;
-                                const uint32_t y = match_src(oj, sj, Lj, r);
-                                if (y + 4 <= oj) {              // 4 contiguous source bytes
-                                    val = y + kRing >= step_end + 4 ? ring_dword(S, y)
-                                                                    : global_dword<true>(k.out + y);
-                                    fast = true;
-                                }
-                            }
-                        }
-                        if (!fast) {
-                            val = 0;
+                        uint32_t gmask = 0;                     // bytes needing global reads
 #pragma unroll
+                        for (uint32_t q = 0; q < 4; q++) {
+                            const uint32_t xb = x + q;
+                            const uint32_t jq = jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u));
+                            const uint32_t oj = S.wo[jq];
+                            const uint32_t sj = S.ws[jq];
+                            const uint32_t mj = S.wm[jq];
+                            const bool litq = (sj & kLitFlag) != 0;
+                            const uint32_t rel = (sj & ~kLitFlag) + (xb - oj) - k.P;
+                            const uint32_t Wj = W > oj ? W : oj;
+                            const uint32_t n = xb - Wj;
+                            const uint32_t m = 1u + (sj == 1 ? n : (uint32_t)__umulhi(n, mj));
+                            const uint32_t y = xb - sj * (mj ? m : 1u);
+                            const bool old = xb < os;
+                            const bool isg = !old && (litq ? rel >= k.staged : y + kRing < step_end + 4);
+                            const uint32_t a = old ? kRingOff + (xb & kRingMask)
+                                             : litq ? kStageOff + (isg ? 0u : rel)
+                                                    : kRingOff + (y & kRingMask);
+                            const uint32_t bv = xb < oe ? (uint32_t)lds[a] : 0u;
+                            val |= bv << (8 * q);
+                            gmask |= (isg && xb < oe) ? (1u << q) : 0u;
+                        }
+                        if (gmask) {                            // literal past staging / far match
                             for (uint32_t q = 0; q < 4; q++) {
+                                if (!(gmask & (1u << q)))
+                                    continue;
                                 const uint32_t xb = x + q;
                                 const uint32_t jq = jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u));
-                                uint32_t bv = 0;
-                                if (xb < os)
-                                    bv = ring_byte(S, xb);     // an earlier batch's byte
-                                else if (xb < oe) {
-                                    const uint32_t oj = S.wo[jq];
-                                    const uint32_t sj = S.ws[jq];
-                                    const uint32_t r = xb - oj;
-                                    if (sj & kLitFlag) {
-                                        const uint32_t ip = (sj & ~kLitFlag) + r;
-                                        const uint32_t rel = ip - k.P;
-                                        bv = rel < k.staged ? stage_byte(S, rel)
-                                                            : (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + ip));
-                                    } else {
-                                        const uint32_t y = match_src(oj, sj, S.wo[jq + 1] - oj, r);
-                                        bv = y + kRing >= step_end + 4 ? ring_byte(S, y)
-                                                                       : global_byte_nt(k.out + y);
-                                    }
+                                const uint32_t oj = S.wo[jq];
+                                const uint32_t sj = S.ws[jq];
+                                const uint32_t mj = S.wm[jq];
+                                uint32_t bv;
+                                if (sj & kLitFlag) {
+                                    const uint32_t ip = (sj & ~kLitFlag) + (xb - oj);
+                                    bv = *((__attribute__((address_space(1))) const uint8_t*)(k.in + ip));
+                                } else {
+                                    const uint32_t Wj = W > oj ? W : oj;
+                                    const uint32_t n = xb - Wj;
+                                    const uint32_t m = 1u + (sj == 1 ? n : (uint32_t)__umulhi(n, mj));
+                                    bv = global_byte_nt(k.out + (xb - sj * (mj ? m : 1u)));
                                 }
-                                val |= bv << (8 * q);
+                                val = (val & ~(0xFFu << (8 * q))) | (bv << (8 * q));
                             }
                         }
                         S.ring[(x & kRingMask) >> 2] = val;
                     }
                     wave_order();
+                    STAMP(PH_GATHER);
                     // bytes below min(step_end, oe) are final: hand them over
                     lds_store(&S.produced, step_end < oe ? step_end : oe);
                     STAMP(PH_STEPS);
@@ -763,8 +846,8 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
     }
 
     if (STAMPS && l == 0)
-        for (int i = 0; i < 8; i++)
-            stamps[(size_t)b * 8 + i] = acc[i];
+        for (int i = 0; i < PH_N; i++)
+            stamps[(size_t)b * 16 + i] = acc[i];
 #undef STAMP
     if (l == 0) {
         if (refuse) {

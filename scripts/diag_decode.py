@@ -29,7 +29,7 @@ zsrc = lzo.DeviceBatch(za, zb.off, zl)
 out = torch.zeros_like(src.arena); ob = lzo.DeviceBatch(out, src.off, src.length)
 ol = torch.zeros_like(zl); os_ = torch.zeros_like(zl)
 fb = torch.zeros(nb + 1, dtype=torch.int32, device=dev)
-stamps = torch.zeros(nb * 8, dtype=torch.int64, device=dev)
+stamps = torch.zeros(nb * 16, dtype=torch.int64, device=dev)
 fn = lib.lzo_mi355x_debug_decompress_fast_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
@@ -50,8 +50,9 @@ for stamp in (False, True):
     e0.record(); run(stamp); e1.record(); torch.cuda.synchronize()
     print(f"stamps={stamp}: kernel {e0.elapsed_time(e1):.3f} ms, fallback {int(fb[0].item())}, "
           f"equal {torch.equal(out, src.arena)}")
-st = stamps.view(nb, 8).double().cpu().numpy()
-names = ["stage", "pass1", "merge", "count", "write", "form", "steps", "walks"]
-tot = st.sum(1)
+st = stamps.view(nb, 16).double().cpu().numpy()
+names = ["stage", "pass1", "merge", "count", "write", "form", "steps(write+publish)", "walks",
+         "space", "flags", "gather", "nstep", "nbatch", "nslow"]
+tot = st[:, [0,1,2,3,4,5,6,8,9,10]].sum(1)
 print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(names)}, "total", int(tot.mean()))
 print("zlen mean", float(zl.double().mean()))
