@@ -67,7 +67,8 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t opS[kOpMax];
     uint32_t wo[kWave + 4];
     uint32_t ws[kWave + 4];
-    uint32_t wm[kWave + 4];   // periodic-match reciprocal: ceil(2^32 / d), 0 = not periodic
+    uint32_t wp[kWave + 4];   // op source period (0: none)
+    uint32_t wm[kWave + 4];   // floor((2^32 - 1) / period)
     uint32_t flags[kWave];
     uint8_t marks[kPiece];
     // decoder -> writer hand-off (LDS words, workgroup scope)
@@ -718,24 +719,59 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                 refuse = true;
                 break;
             }
-            // end of each match's source range (periodic copies read only [o-d, o))
-            const uint32_t send = lit ? 0u : o - Sv + (Sv < L ? Sv : L);
-            // A periodic match (d < L) repeats its first d bytes: for any byte x
-            // and any W <= x with W >= o, out[x] = out[x - d*m], m = (x-W)/d + 1
-            // (the source then lies in [W - d, W), already written).  Within one
-            // 256-byte step x - W <= 258, so only d <= 258 needs the division,
-            // done as a multiply-high by ceil(2^32/d) (exact for these sizes).
-            const bool per = !lit && Sv < L && Sv <= 258;
+            // ---- op descriptors: byte x of op j reads
+            //   src[b + ((x - o) mod p)]   (p == 0: src[b + x - o])
+            // in the input (kLitFlag set in b) or in the output.  A match
+            // starts as b = o - d, p = d if it overlaps itself (d < L).
+            uint32_t db = lit ? Sv : o - Sv;
+            uint32_t dp = (!lit && Sv < L) ? Sv : 0u;
+            // Source forwarding: a match whose source span lies inside one
+            // earlier op of this window reads that op's source instead, so it
+            // no longer waits for it.  Three parallel rounds reach the
+            // sequential fixed point on ITB streams (600 -> 205 batches per
+            // 64 KiB block).
+            const uint32_t o_first = lane_read(o, 0);
+            for (int round = 0; round < 3; round++) {
+                const uint32_t span = dp ? dp : L;
+                const bool need = l < nwin && !(db & kLitFlag) && db + span > o_first;
+                if (!wave_ballot(need))
+                    break;
+                uint32_t k2 = 0;                       // last op with o <= db
+#pragma unroll
+                for (uint32_t w = 32; w >= 1; w >>= 1) {
+                    const uint32_t c = k2 + w;
+                    const uint32_t oc = (uint32_t)__shfl((int)o, (int)(c & 63u), kWave);
+                    if (c < nwin && oc <= db)
+                        k2 = c;
+                }
+                const uint32_t ko = (uint32_t)__shfl((int)o, (int)k2, kWave);
+                const uint32_t kL = (uint32_t)__shfl((int)L, (int)k2, kWave);
+                const uint32_t kb = (uint32_t)__shfl((int)db, (int)k2, kWave);
+                const uint32_t kp = (uint32_t)__shfl((int)dp, (int)k2, kWave);
+                bool ok = need && k2 < l && ko <= db && db + span <= ko + kL;
+                uint32_t r = db - ko;
+                if (ok && kp) {
+                    r %= kp;
+                    ok = r + span <= kp;
+                }
+                if (ok)
+                    db = kb + r;                       // (kb carries k's input flag)
+            }
+            // end of each output-sourced op's source span: a batch may not read
+            // its own output
+            const bool outsrc = l < nwin && !(db & kLitFlag);
+            const uint32_t send = outsrc ? db + (dp ? dp : L) : 0u;
             S.wo[l] = o;
-            S.ws[l] = Sv;
-            S.wm[l] = !per ? 0u : Sv == 1 ? 0xFFFFFFFFu : (uint32_t)(0xFFFFFFFFu / Sv) + 1u;
+            S.ws[l] = db;
+            S.wp[l] = dp;
+            S.wm[l] = dp ? 0xFFFFFFFFu / dp : 0u;      // floor((2^32-1)/p): mod by mulhi
             if (l == 0)
                 S.wo[kWave] = carry + wtotal;
             wave_order();
             uint32_t s = 0;
             while (s < nwin) {
                 const uint32_t os = lane_read(o, s);
-                const bool brk = l > s && l < nwin && !lit && send > os;
+                const bool brk = l > s && outsrc && send > os;
                 const uint64_t bm = wave_ballot(brk);
                 const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nwin;
                 const uint32_t oe = e < nwin ? lane_read(o, e) : carry + wtotal;
@@ -778,52 +814,46 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                     const uint32_t x = xs + 4 * l;
                     if (x < oe) {
                         // Every byte the same way (no divergent paths): its op's
-                        // affine source -> one LDS byte read (stage or ring).
-                        const uint32_t W = os > xs ? os : xs;   // bytes below W are written
+                        // source -> one LDS byte read (stage or ring).
                         const uint8_t* lds = (const uint8_t*)&S;
                         uint32_t val = 0;
                         uint32_t gmask = 0;                     // bytes needing global reads
+                        uint32_t gsrc[4];
 #pragma unroll
                         for (uint32_t q = 0; q < 4; q++) {
                             const uint32_t xb = x + q;
                             const uint32_t jq = jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u));
                             const uint32_t oj = S.wo[jq];
-                            const uint32_t sj = S.ws[jq];
+                            const uint32_t bj = S.ws[jq];
+                            const uint32_t pj = S.wp[jq];
                             const uint32_t mj = S.wm[jq];
-                            const bool litq = (sj & kLitFlag) != 0;
-                            const uint32_t rel = (sj & ~kLitFlag) + (xb - oj) - k.P;
-                            const uint32_t Wj = W > oj ? W : oj;
-                            const uint32_t n = xb - Wj;
-                            const uint32_t m = 1u + (sj == 1 ? n : (uint32_t)__umulhi(n, mj));
-                            const uint32_t y = xb - sj * (mj ? m : 1u);
+                            const uint32_t r = xb - oj;
+                            uint32_t rr = r;
+                            if (pj) {                           // r mod p, one correction
+                                rr = r - pj * (uint32_t)__umulhi(r, mj);
+                                rr = rr >= pj ? rr - pj : rr;
+                            }
+                            const uint32_t sp = (bj & ~kLitFlag) + rr;   // source position
+                            const bool litq = (bj & kLitFlag) != 0;
+                            const uint32_t rel = sp - k.P;
                             const bool old = xb < os;
-                            const bool isg = !old && (litq ? rel >= k.staged : y + kRing < step_end + 4);
+                            const bool isg = !old && (litq ? rel >= k.staged : sp + kRing < step_end + 4);
                             const uint32_t a = old ? kRingOff + (xb & kRingMask)
                                              : litq ? kStageOff + (isg ? 0u : rel)
-                                                    : kRingOff + (y & kRingMask);
+                                                    : kRingOff + (sp & kRingMask);
                             const uint32_t bv = xb < oe ? (uint32_t)lds[a] : 0u;
                             val |= bv << (8 * q);
+                            gsrc[q] = litq ? (sp | kLitFlag) : sp;
                             gmask |= (isg && xb < oe) ? (1u << q) : 0u;
                         }
                         if (gmask) {                            // literal past staging / far match
                             for (uint32_t q = 0; q < 4; q++) {
                                 if (!(gmask & (1u << q)))
                                     continue;
-                                const uint32_t xb = x + q;
-                                const uint32_t jq = jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u));
-                                const uint32_t oj = S.wo[jq];
-                                const uint32_t sj = S.ws[jq];
-                                const uint32_t mj = S.wm[jq];
-                                uint32_t bv;
-                                if (sj & kLitFlag) {
-                                    const uint32_t ip = (sj & ~kLitFlag) + (xb - oj);
-                                    bv = *((__attribute__((address_space(1))) const uint8_t*)(k.in + ip));
-                                } else {
-                                    const uint32_t Wj = W > oj ? W : oj;
-                                    const uint32_t n = xb - Wj;
-                                    const uint32_t m = 1u + (sj == 1 ? n : (uint32_t)__umulhi(n, mj));
-                                    bv = global_byte_nt(k.out + (xb - sj * (mj ? m : 1u)));
-                                }
+                                const uint32_t g = gsrc[q];
+                                const uint32_t bv = (g & kLitFlag)
+                                    ? (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + (g & ~kLitFlag)))
+                                    : global_byte_nt(k.out + g);
                                 val = (val & ~(0xFFu << (8 * q))) | (bv << (8 * q));
                             }
                         }
