@@ -65,10 +65,7 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t stage[kStageBytes / 4];
     uint32_t opL[kOpMax];
     uint32_t opS[kOpMax];
-    uint32_t wo[kWave + 4];
-    uint32_t ws[kWave + 4];
-    uint32_t wp[kWave + 4];   // op source period (0: none)
-    uint32_t wm[kWave + 4];   // floor((2^32 - 1) / period)
+    uint4 wop[kWave + 4];     // per window op: {o, source base (| kLitFlag), period, floor((2^32-1)/period)}
     uint32_t flags[kWave];
     uint8_t marks[kPiece];
     // decoder -> writer hand-off (LDS words, workgroup scope)
@@ -761,12 +758,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
             // its own output
             const bool outsrc = l < nwin && !(db & kLitFlag);
             const uint32_t send = outsrc ? db + (dp ? dp : L) : 0u;
-            S.wo[l] = o;
-            S.ws[l] = db;
-            S.wp[l] = dp;
-            S.wm[l] = dp ? 0xFFFFFFFFu / dp : 0u;      // floor((2^32-1)/p): mod by mulhi
-            if (l == 0)
-                S.wo[kWave] = carry + wtotal;
+            S.wop[l] = make_uint4(o, db, dp, dp ? 0xFFFFFFFFu / dp : 0u);   // mod by mulhi
             wave_order();
             uint32_t s = 0;
             while (s < nwin) {
@@ -813,38 +805,38 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                     STAMP(PH_FLAGS);
                     const uint32_t x = xs + 4 * l;
                     if (x < oe) {
-                        // Every byte the same way (no divergent paths): its op's
-                        // source -> one LDS byte read (stage or ring).
+                        // Every byte the same way, branch-free: its op record (one
+                        // 16-byte LDS read), then its source byte (one LDS read).
                         const uint8_t* lds = (const uint8_t*)&S;
-                        uint32_t val = 0;
+                        uint4 op[4];
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; q++)
+                            op[q] = S.wop[jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u))];
+                        uint32_t addr[4], gsrc[4];
                         uint32_t gmask = 0;                     // bytes needing global reads
-                        uint32_t gsrc[4];
 #pragma unroll
                         for (uint32_t q = 0; q < 4; q++) {
                             const uint32_t xb = x + q;
-                            const uint32_t jq = jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u));
-                            const uint32_t oj = S.wo[jq];
-                            const uint32_t bj = S.ws[jq];
-                            const uint32_t pj = S.wp[jq];
-                            const uint32_t mj = S.wm[jq];
-                            const uint32_t r = xb - oj;
-                            uint32_t rr = r;
-                            if (pj) {                           // r mod p, one correction
-                                rr = r - pj * (uint32_t)__umulhi(r, mj);
-                                rr = rr >= pj ? rr - pj : rr;
-                            }
-                            const uint32_t sp = (bj & ~kLitFlag) + rr;   // source position
-                            const bool litq = (bj & kLitFlag) != 0;
+                            const uint32_t r = xb - op[q].x;
+                            uint32_t rr = r - op[q].z * (uint32_t)__umulhi(r, op[q].w);  // r mod p
+                            rr -= rr >= op[q].z ? op[q].z : 0u;  // (p == 0: rr = r)
+                            const uint32_t sp = (op[q].y & ~kLitFlag) + rr;
+                            const bool litq = (op[q].y & kLitFlag) != 0;
                             const uint32_t rel = sp - k.P;
                             const bool old = xb < os;
-                            const bool isg = !old && (litq ? rel >= k.staged : sp + kRing < step_end + 4);
-                            const uint32_t a = old ? kRingOff + (xb & kRingMask)
-                                             : litq ? kStageOff + (isg ? 0u : rel)
-                                                    : kRingOff + (sp & kRingMask);
-                            const uint32_t bv = xb < oe ? (uint32_t)lds[a] : 0u;
-                            val |= bv << (8 * q);
+                            const bool live = !old && xb < oe;
+                            const bool isg = live && (litq ? rel >= k.staged : sp + kRing < step_end + 4);
+                            const uint32_t ring_a = kRingOff + ((old ? xb : sp) & kRingMask);
+                            const uint32_t stage_a = kStageOff + (rel < k.staged ? rel : 0u);
+                            addr[q] = (litq && !old) ? stage_a : ring_a;
                             gsrc[q] = litq ? (sp | kLitFlag) : sp;
-                            gmask |= (isg && xb < oe) ? (1u << q) : 0u;
+                            gmask |= isg ? (1u << q) : 0u;
+                        }
+                        uint32_t val = 0;
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; q++) {
+                            const uint32_t keep = x + q < oe ? 0xFFu : 0u;
+                            val |= ((uint32_t)lds[addr[q]] & keep) << (8 * q);
                         }
                         if (gmask) {                            // literal past staging / far match
                             for (uint32_t q = 0; q < 4; q++) {
