@@ -46,7 +46,10 @@ constexpr uint32_t kLook = 24;                   // speculative lead-in before a
 constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
 constexpr uint32_t kOpMax = 512;                 // ops per piece
-constexpr uint32_t kRing = 16384;                // recent output kept in LDS
+#ifndef POM_RING
+#define POM_RING 8192
+#endif
+constexpr uint32_t kRing = POM_RING;             // recent output kept in LDS
 constexpr uint32_t kRingSlack = 1024;            // decoder keeps this much ring unflushed-free
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kLitFlag = 0x80000000u;
@@ -59,6 +62,7 @@ constexpr uint32_t ST_B = 1;   // after a literal run: t < 16 is a 3-byte M1 (di
 constexpr uint32_t ST_C = 2;   // after trailing literals: t < 16 is a 2-byte M1
 constexpr uint32_t ST_F = 3;   // first byte of the stream (lib/minilzo.c:3357)
 constexpr uint32_t kPosEnd = 0xFFFFFFF0u;        // exit marker: EOF reached / dead path
+constexpr uint32_t kPosUnknown = 0xFFFFFFE0u;    // speculative walk gave up
 
 struct __attribute__((aligned(16))) FastLds {
     uint32_t ring[kRing / 4];
@@ -260,11 +264,26 @@ __device__ __noinline__ Step decode_one(const FastLds& s, const Blk& k, uint32_t
 // LDS round trip (three aligned dwords -> 8 bytes at pos), then selects; lanes
 // decoding different instruction kinds do not diverge.  Falls back to
 // decode_one otherwise (long extensions, input beyond the staging window).
-__device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st)
+// SPEC: speculative use -- never take the slow path; report it as `slow`
+// (the caller restarts or re-walks exactly) instead.
+template <bool SPEC = false>
+__device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st,
+                                            bool* slow = nullptr)
 {
     const uint32_t rel = pos - k.P;
-    if (rel + 12 > kStageBytes || pos >= k.z)
+    if (rel + 12 > kStageBytes || pos >= k.z) {
+        if (SPEC) {
+            Step r;
+            r.pos = pos;
+            r.st = st;
+            r.aL = r.aS = r.bL = r.bS = 0;
+            r.eof = false;
+            r.bad = true;
+            *slow = true;
+            return r;
+        }
         return decode_one(s, k, pos, st);
+    }
     const uint32_t w0 = s.stage[rel >> 2], w1 = s.stage[(rel >> 2) + 1], w2 = s.stage[(rel >> 2) + 2];
     const uint32_t sh = 8u * (rel & 3u);
     const uint64_t lo64 = ((uint64_t)w1 << 32) | w0;
@@ -291,8 +310,17 @@ __device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint
     const bool lit = se == ST_A && t < 16;
     const bool ext = (lit && t == 0) || (t >= 32 && t < 64 && (t & 31) == 0) ||
                      (t >= 16 && t < 32 && (t & 7) == 0);
-    if (ext && b1 == 0)
-        return decode_one(s, k, pos, st);                          // 255-chunk extension
+    if (ext && b1 == 0) {                                          // 255-chunk extension
+        if (SPEC) {
+            r.pos = pos;
+            r.st = st;
+            r.aL = r.aS = 0;
+            r.bad = true;
+            *slow = true;
+            return r;
+        }
+        return decode_one(s, k, pos, st);
+    }
     const uint32_t e = ext ? 1u : 0u;
     if (lit) {                                                     // :3367-3414
         const uint32_t n = (ext ? 15u + b1 : t) + 3u;
@@ -395,6 +423,9 @@ enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_W
 // Uniform walk of the true path from (pos, st) through lane i's segment
 // [c0, c1) until it lands on one of lane i's final-generation marks (then
 // lane i's speculative exit is the answer) or leaves the segment.
+// SPEC: per-lane speculative walk that gives up (pos = kPosUnknown) where the
+// exact slow decoder would be needed; the scalar scan then walks exactly.
+template <bool SPEC>
 __device__ __forceinline__ void walk_uniform(const FastLds& S, const Blk& k, uint32_t c0,
                                              uint32_t c1, uint32_t gen, uint32_t xpos,
                                              uint32_t xst, uint32_t& pos, uint32_t& st)
@@ -410,7 +441,13 @@ __device__ __forceinline__ void walk_uniform(const FastLds& S, const Blk& k, uin
             st = xst;
             return;
         }
-        const Step r = decode_step(S, k, pos, st);
+        bool slow = false;
+        const Step r = decode_step<SPEC>(S, k, pos, st, &slow);
+        if (SPEC && slow) {
+            pos = kPosUnknown;
+            st = 0;
+            return;
+        }
         if (r.bad || r.eof) {
             pos = kPosEnd;
             st = 0;
@@ -431,7 +468,7 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
 {
     constexpr uint32_t kChunk = 16 * kWave;        // 1 KiB per store instruction
     uint32_t issued = 0;
-    uint32_t pend[4] = {0, 0, 0, 0};               // ends of chunks in flight, oldest first
+    uint32_t pend[2] = {0, 0};                     // ends of chunks in flight, oldest first
     uint32_t npend = 0;
     for (uint32_t spin = 0; spin < (1u << 24); spin++) {
         const uint32_t state = lds_load(&S.state);
@@ -451,13 +488,11 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
                     out[x + q] = (uint8_t)ring_byte(S, x + q);
             }
             issued = end;
-            if (npend == 4) {
-                __builtin_amdgcn_s_waitcnt(0x0F73);        // vmcnt(3): oldest chunk landed
+            if (npend == 2) {
+                __builtin_amdgcn_s_waitcnt(0x0F71);        // vmcnt(1): oldest chunk landed
                 lds_store(&S.flushed, pend[0]);
                 pend[0] = pend[1];
-                pend[1] = pend[2];
-                pend[2] = pend[3];
-                npend = 3;
+                npend = 1;
             }
             pend[npend++] = end;
             continue;
@@ -576,7 +611,8 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
             while (pos < c1 && pos < k.z) {
                 if (pos >= c0)
                     S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 2));
-                const Step r = decode_step(S, k, pos, st);
+                bool slow = false;
+                const Step r = decode_step<true>(S, k, pos, st, &slow);
                 if (r.bad || r.eof) {                  // impossible guess: restart later
                     pos++;
                     st = ST_A;
@@ -597,7 +633,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
         // scalar scan that reuses it and walks only where the guess was wrong.
         const uint32_t apos = shift_up1(xpos, entry_pos), ast = shift_up1(xst, entry_st);
         uint32_t fpos = apos, fst = ast;
-        walk_uniform(S, k, c0, c1, xgen, xpos, xst, fpos, fst);   // per lane (divergent)
+        walk_uniform<true>(S, k, c0, c1, xgen, xpos, xst, fpos, fst);   // per lane (divergent)
         uint32_t epos = 0, est = 0;
         {
             uint32_t E = entry_pos, Est = entry_st;
@@ -609,13 +645,14 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                 const uint32_t ci1 = k.P + (i + 1) * kSeg;
                 if (E >= ci1)
                     continue;                          // segment i has no true start
-                if (E == lane_read(apos, i) && Est == lane_read(ast, i)) {
+                if (E == lane_read(apos, i) && Est == lane_read(ast, i) &&
+                    lane_read(fpos, i) != kPosUnknown) {
                     E = lane_read(fpos, i);
                     Est = lane_read(fst, i);
                     continue;
                 }
-                walk_uniform(S, k, ci1 - kSeg, ci1, lane_read(xgen, i), lane_read(xpos, i),
-                             lane_read(xst, i), E, Est);
+                walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i), lane_read(xpos, i),
+                                    lane_read(xst, i), E, Est);
                 if (STAMPS)
                     acc[PH_WALKS] += 1;
             }
