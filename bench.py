@@ -162,11 +162,16 @@ def main():
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the LZO1X path has no CPU fallback)")
-    dev = torch.device(f"cuda:{local}")
+    # One process per GPU.  POM_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs.
+    backend = os.environ.get("POM_DIST_BACKEND", "nccl")
+    dev = torch.device(f"cuda:{local % torch.cuda.device_count()}")
     torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     lzo.load()
 
     model = {v: k for k, v in synth.MODEL_NAMES.items()}[args.model]
@@ -232,7 +237,8 @@ def main():
     if world > 1:
         errors, dec_wall = shard.completion_barrier(dist, dev, errors, dec_wall)
         _, comp_wall = shard.completion_barrier(dist, dev, 0, comp_wall)
-        tot = torch.tensor([n_bytes, z_bytes], dtype=torch.float64, device=dev)
+        tot = torch.tensor([n_bytes, z_bytes], dtype=torch.float64,
+                           device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tot)
         n_all, z_all = float(tot[0].item()), float(tot[1].item())
     else:

@@ -29,6 +29,8 @@ def per_rank_bytes(sizes: Sequence[int], world: int) -> List[int]:
 def completion_barrier(dist, device, errors: int, elapsed_s: float) -> Tuple[int, float]:
     """All-reduce (sum errors, max elapsed) over the process group."""
     import torch
+    if dist.get_backend() == "gloo":            # gloo collectives run on host tensors
+        device = torch.device("cpu")
     t = torch.tensor([float(errors)], dtype=torch.float64, device=device)
     e = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
