@@ -41,11 +41,17 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr uint32_t kSeg = 16;                    // input bytes per lane per piece
-constexpr uint32_t kLook = 24;                   // speculative lead-in before a segment
+#ifndef POM_SEG
+#define POM_SEG 16
+#endif
+#ifndef POM_LOOK
+#define POM_LOOK 24
+#endif
+constexpr uint32_t kSeg = POM_SEG;               // input bytes per lane per piece
+constexpr uint32_t kLook = POM_LOOK;             // speculative lead-in before a segment
 constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
-constexpr uint32_t kOpMax = 512;                 // ops per piece
+constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
 #ifndef POM_RING
 #define POM_RING 8192
 #endif
