@@ -52,6 +52,9 @@ constexpr uint32_t kLook = POM_LOOK;             // speculative lead-in before a
 constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
 constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
+#ifndef POM_WRITER_SLEEP
+#define POM_WRITER_SLEEP 24                      // ~1.5K cycles between writer polls
+#endif
 #ifndef POM_RING
 #define POM_RING 8192
 #endif
@@ -476,7 +479,7 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
     uint32_t issued = 0;
     uint32_t pend[2] = {0, 0};                     // ends of chunks in flight, oldest first
     uint32_t npend = 0;
-    for (uint32_t spin = 0; spin < (1u << 24); spin++) {
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
         const uint32_t state = lds_load(&S.state);
         const uint32_t prod = lds_load(&S.produced);
         if (state == 2)
@@ -511,7 +514,9 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
         }
         if (state == 1)
             return;
-        __builtin_amdgcn_s_sleep(2);
+        // Poll rarely: the scalar unit is shared by every wave of the CU, and a
+        // tight poll loop costs the decoder waves their SALU issue slots.
+        __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
     }
 }
 
