@@ -53,7 +53,7 @@ constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
 constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
 #ifndef POM_WRITER_SLEEP
-#define POM_WRITER_SLEEP 24                      // ~1.5K cycles between writer polls
+#define POM_WRITER_SLEEP 40                      // ~1.5K cycles between writer polls
 #endif
 #ifndef POM_RING
 #define POM_RING 8192
@@ -280,96 +280,63 @@ __device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint
                                             bool* slow = nullptr)
 {
     const uint32_t rel = pos - k.P;
-    if (rel + 12 > kStageBytes || pos >= k.z) {
-        if (SPEC) {
-            Step r;
-            r.pos = pos;
-            r.st = st;
-            r.aL = r.aS = r.bL = r.bS = 0;
-            r.eof = false;
-            r.bad = true;
-            *slow = true;
-            return r;
-        }
-        return decode_one(s, k, pos, st);
-    }
-    const uint32_t w0 = s.stage[rel >> 2], w1 = s.stage[(rel >> 2) + 1], w2 = s.stage[(rel >> 2) + 2];
+    const bool inwin = rel + 12 <= kStageBytes && pos < k.z;
+    // The 8 bytes at pos (read unconditionally from a clamped window offset;
+    // ignored when !inwin).
+    const uint32_t wi = inwin ? rel >> 2 : 0u;
+    const uint32_t w0 = s.stage[wi], w1 = s.stage[wi + 1], w2 = s.stage[wi + 2];
     const uint32_t sh = 8u * (rel & 3u);
-    const uint64_t lo64 = ((uint64_t)w1 << 32) | w0;
-    const uint32_t lo = (uint32_t)(lo64 >> sh);
+    const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
     const uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
     const uint64_t b8 = ((uint64_t)hi << 32) | lo;                 // bytes pos..pos+7
 #define BYTE(i) ((uint32_t)(b8 >> (8u * (i))) & 0xFFu)
     const uint32_t t = lo & 0xFFu, b1 = BYTE(1);
-    Step r;
-    r.eof = false;
-    r.bL = r.bS = 0;
-    const bool first = st == ST_F;
-    if (first && t > 17) {                                         // :3357-3365
-        const uint32_t n = t - 17;
-        r.aL = n;
-        r.aS = kLitFlag | (pos + 1);
-        r.pos = pos + 1 + n;
-        r.st = n < 4 ? ST_C : ST_B;
-        r.bad = r.pos > k.z;
-        return r;
-    }
-    const uint32_t se = first ? ST_A : st;
-    // extension byte needed: literal run t == 0, M3 with t&31 == 0, M4 with t&7 == 0
-    const bool lit = se == ST_A && t < 16;
-    const bool ext = (lit && t == 0) || (t >= 32 && t < 64 && (t & 31) == 0) ||
-                     (t >= 16 && t < 32 && (t & 7) == 0);
-    if (ext && b1 == 0) {                                          // 255-chunk extension
-        if (SPEC) {
-            r.pos = pos;
-            r.st = st;
-            r.aL = r.aS = 0;
-            r.bad = true;
-            *slow = true;
-            return r;
-        }
-        return decode_one(s, k, pos, st);
-    }
+    const bool flit = st == ST_F && t > 17;                        // :3357-3365
+    const uint32_t se = st == ST_F ? ST_A : st;
+    const bool lit = !flit && se == ST_A && t < 16;                // :3367-3414
+    const bool m1 = !flit && !lit && t < 16;
+    const bool m2 = !flit && t >= 64;
+    const bool m3 = !flit && t >= 32 && t < 64;
+    const bool m4 = !flit && t >= 16 && t < 32;
+    const bool ext = (lit && t == 0) || (m3 && (t & 31) == 0) || (m4 && (t & 7) == 0);
+    const bool needs_slow = !inwin || (ext && b1 == 0);            // 255-chunk extension
     const uint32_t e = ext ? 1u : 0u;
-    if (lit) {                                                     // :3367-3414
-        const uint32_t n = (ext ? 15u + b1 : t) + 3u;
-        r.aL = n;
-        r.aS = kLitFlag | (pos + 1 + e);
-        r.pos = pos + 1 + e + n;
-        r.st = ST_B;
-        r.bad = r.pos > k.z;
-        return r;
-    }
-    // matches: M1 (t < 16), M2 (t >= 64), M3 (32..63), M4 (16..31)
     const uint32_t o16 = BYTE(1 + e) | (BYTE(2 + e) << 8);
-    const uint32_t dm1 = (se == ST_B ? 0x801u : 1u) + (t >> 2) + (b1 << 2);
-    const uint32_t dm2 = 1u + ((t >> 2) & 7u) + (b1 << 3);
-    const uint32_t dm3 = 1u + (o16 >> 2);
     const uint32_t dd4 = ((t & 8u) << 11) + (o16 >> 2);
-    const bool m1 = t < 16, m2 = t >= 64, m3 = t >= 32 && t < 64;
+    const uint32_t used = (m1 || m2) ? 2u : 3u + e;                // match instruction bytes
+    const uint32_t tl = BYTE(used - 2) & 3u;                       // match_done, :3650
+#undef BYTE
+    const uint32_t nlit = flit ? t - 17 : (ext ? 15u + b1 : t) + 3u;
     const uint32_t L = m1 ? (se == ST_B ? 3u : 2u)
                      : m2 ? (t >> 5) + 1u
                      : m3 ? (ext ? 31u + b1 : (t & 31u)) + 2u
                           : (ext ? 7u + b1 : (t & 7u)) + 2u;
-    const uint32_t d = m1 ? dm1 : m2 ? dm2 : m3 ? dm3 : dd4 + 0x4000u;
-    const uint32_t used = (m1 || m2) ? 2u : 3u + e;
-    if (!m1 && !m2 && !m3 && dd4 == 0) {                           // EOF, :3580
-        r.eof = true;
-        r.pos = pos + used;
-        r.st = ST_A;
-        r.aL = r.aS = 0;
-        r.bad = r.pos != k.z;
-        return r;
-    }
-    const uint32_t tl = BYTE(used - 2) & 3u;                       // match_done, :3650
-#undef BYTE
-    r.aL = L;
-    r.aS = d;
-    r.bL = tl;
+    const uint32_t d = m1 ? (se == ST_B ? 0x801u : 1u) + (t >> 2) + (b1 << 2)
+                     : m2 ? 1u + ((t >> 2) & 7u) + (b1 << 3)
+                     : m3 ? 1u + (o16 >> 2) : dd4 + 0x4000u;
+    const bool eof = m4 && dd4 == 0;                               // :3580
+    const bool islit = flit || lit;
+    const uint32_t hdr = flit ? 1u : 1u + e;                       // literal-run header bytes
+    Step r;
+    r.eof = eof;
+    r.aL = eof ? 0u : islit ? nlit : L;
+    r.aS = islit ? kLitFlag | (pos + hdr) : d;
+    r.bL = (islit || eof) ? 0u : tl;
     r.bS = kLitFlag | (pos + used);
-    r.pos = pos + used + tl;
-    r.st = tl ? ST_C : ST_A;
-    r.bad = r.pos > k.z;
+    r.pos = islit ? pos + hdr + nlit : pos + used + (eof ? 0u : tl);
+    r.st = islit ? (flit && nlit < 4 ? ST_C : ST_B) : (tl && !eof ? ST_C : ST_A);
+    r.bad = eof ? r.pos != k.z : r.pos > k.z;
+    if (__builtin_expect(needs_slow, 0)) {
+        if (SPEC) {
+            r.pos = pos;
+            r.st = st;
+            r.aL = r.bL = 0;
+            r.eof = false;
+            r.bad = true;
+            *slow = true;
+        } else
+            r = decode_one(s, k, pos, st);
+    }
     return r;
 }
 
@@ -852,7 +819,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                     jcarry += lane_read(sincl, kWave - 1);
                     STAMP(PH_FLAGS);
                     const uint32_t x = xs + 4 * l;
-                    if (x < oe) {
+                    {
                         // Every byte the same way, branch-free: its op record (one
                         // 16-byte LDS read), then its source byte (one LDS read).
                         const uint8_t* lds = (const uint8_t*)&S;
@@ -886,7 +853,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                             const uint32_t keep = x + q < oe ? 0xFFu : 0u;
                             val |= ((uint32_t)lds[addr[q]] & keep) << (8 * q);
                         }
-                        if (gmask) {                            // literal past staging / far match
+                        if (wave_ballot(gmask != 0)) {          // literal past staging / far match
                             for (uint32_t q = 0; q < 4; q++) {
                                 if (!(gmask & (1u << q)))
                                     continue;
