@@ -55,11 +55,14 @@ constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
 #ifndef POM_WRITER_SLEEP
 #define POM_WRITER_SLEEP 40                      // ~1.5K cycles between writer polls
 #endif
+#ifndef POM_WAVES_PER_EU
+#define POM_WAVES_PER_EU 8                       // 16 blocks (decoder + writer wave) per CU
+#endif
 #ifndef POM_RING
-#define POM_RING 8192
+#define POM_RING 4096
 #endif
 constexpr uint32_t kRing = POM_RING;             // recent output kept in LDS
-constexpr uint32_t kRingSlack = 1024;            // decoder keeps this much ring unflushed-free
+constexpr uint32_t kRingSlack = kRing / 4;       // decoder keeps this much ring unflushed-free
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kLitFlag = 0x80000000u;
 constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wrap 32 bits
@@ -76,11 +79,13 @@ constexpr uint32_t kPosUnknown = 0xFFFFFFE0u;    // speculative walk gave up
 struct __attribute__((aligned(16))) FastLds {
     uint32_t ring[kRing / 4];
     uint32_t stage[kStageBytes / 4];
-    uint32_t opL[kOpMax];
-    uint32_t opS[kOpMax];
+
     uint4 wop[kWave + 4];     // per window op: {o, source base (| kLitFlag), period, floor((2^32-1)/period)}
     uint32_t flags[kWave];
-    uint8_t marks[kPiece];
+    union {
+        uint8_t marks[kPiece];        // parse: speculative path marks (pass 1, merge)
+        uint32_t opref[kOpMax];       // then: the piece's ops as instruction references
+    };
     // decoder -> writer hand-off (LDS words, workgroup scope)
     uint32_t produced;      // output bytes final in the ring
     uint32_t flushed;       // output bytes stored to HBM and landed
@@ -489,7 +494,7 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
 
 // ---------------------------------------------------------------------------
 template <bool STAMPS>
-__global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
+__global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
@@ -683,16 +688,15 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
                 const Step r = decode_step(S, k, pos, st);
                 if (r.eof)
                     break;
-                if (r.aL) {
-                    S.opL[w] = r.aL;
-                    S.opS[w] = r.aS;
-                    w++;
-                }
-                if (r.bL) {
-                    S.opL[w] = r.bL;
-                    S.opS[w] = r.bS;
-                    w++;
-                }
+                // An op is stored as a reference to its instruction
+                // (piece offset | state << 16 | part << 18, part 1 = trailing
+                // literals) and re-decoded when its window executes: 4 bytes
+                // of LDS instead of 8.
+                const uint32_t ref = (pos - k.P) | (st << 16);
+                if (r.aL)
+                    S.opref[w++] = ref;
+                if (r.bL)
+                    S.opref[w++] = ref | (1u << 18);
                 pos = r.pos;
                 st = r.st;
             }
@@ -715,8 +719,11 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_decode_fast_kernel(
             const uint32_t nwin = total_ops - w0 < (uint32_t)kWave ? total_ops - w0 : (uint32_t)kWave;
             uint32_t L = 0, Sv = 0;
             if (l < nwin) {
-                L = S.opL[w0 + l];
-                Sv = S.opS[w0 + l];
+                const uint32_t ref = S.opref[w0 + l];
+                const Step r = decode_step(S, k, k.P + (ref & 0xFFFFu), (ref >> 16) & 3u);
+                const bool part = (ref >> 18) != 0;
+                L = part ? r.bL : r.aL;
+                Sv = part ? r.bS : r.aS;
             }
             const uint32_t inc = wave_incl_scan(L);
             const uint32_t o = carry + inc - L;
