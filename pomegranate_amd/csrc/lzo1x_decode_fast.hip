@@ -860,6 +860,9 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                             const uint32_t keep = x + q < oe ? 0xFFu : 0u;
                             val |= ((uint32_t)lds[addr[q]] & keep) << (8 * q);
                         }
+#ifdef POM_NOFAR_TIMING_ONLY
+                        gmask = 0;                              // timing experiment: wrong output
+#endif
                         if (wave_ballot(gmask != 0)) {          // literal past staging / far match
                             for (uint32_t q = 0; q < 4; q++) {
                                 if (!(gmask & (1u << q)))
