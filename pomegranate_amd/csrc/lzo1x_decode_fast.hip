@@ -64,6 +64,12 @@ constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
 constexpr uint32_t kRing = POM_RING;             // recent output kept in LDS
 constexpr uint32_t kRingSlack = kRing / 4;       // decoder keeps this much ring unflushed-free
 constexpr uint32_t kRingMask = kRing - 1;
+#ifndef POM_FAR
+#define POM_FAR 1024
+#endif
+constexpr uint32_t kFarBytes = POM_FAR;          // per-window copy of far match sources
+constexpr uint32_t kFarDw = kFarBytes / 4;
+static_assert(kFarDw <= 4 * kWave, "far copy: at most 4 dwords per lane");
 constexpr uint32_t kLitFlag = 0x80000000u;
 constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wrap 32 bits
 constexpr int32_t kFallback = 0x7FFF0001;        // status: exact decoder pending
@@ -78,6 +84,7 @@ constexpr uint32_t kPosUnknown = 0xFFFFFFE0u;    // speculative walk gave up
 
 struct __attribute__((aligned(16))) FastLds {
     uint32_t ring[kRing / 4];
+    uint32_t far[kFarDw];     // sources of this window's far matches (beyond the ring)
     uint32_t stage[kStageBytes / 4];
 
     uint4 wop[kWave + 4];     // per window op: {o, source base (| kLitFlag), period, floor((2^32-1)/period)}
@@ -93,9 +100,13 @@ struct __attribute__((aligned(16))) FastLds {
 };
 
 constexpr uint32_t kRingOff = 0;                                  // offsetof(FastLds, ring)
-constexpr uint32_t kStageOff = kRing;                             // offsetof(FastLds, stage)
+constexpr uint32_t kFarOff = kRing;                               // offsetof(FastLds, far)
+constexpr uint32_t kStageOff = kRing + kFarBytes;                 // offsetof(FastLds, stage)
 static_assert(offsetof(FastLds, ring) == kRingOff, "layout");
+static_assert(offsetof(FastLds, far) == kFarOff, "layout");
 static_assert(offsetof(FastLds, stage) == kStageOff, "layout");
+// 16 blocks per CU share its 160 KiB of LDS
+static_assert(sizeof(FastLds) * 2 * POM_WAVES_PER_EU <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
@@ -493,6 +504,94 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
 }
 
 // ---------------------------------------------------------------------------
+// Far sources.  A match whose source may have left the ring by the time its
+// step runs would read HBM byte by byte in every step it touches (61% of the
+// steps of an ITB block).  Instead its whole source span is copied once per
+// window into S.far -- one batched global round trip -- and the op becomes an
+// LDS-linear source like a literal.  Called after forwarding, with the window
+// ops' output offset o, length L, period dp and source b (in/out).
+//
+// Where the bytes are at this point (carry = output before this window): the
+// last step of the previous window ended at most 255 bytes past carry, so the
+// ring still holds every position >= carry + 255 - kRing, and its space check
+// left flushed >= carry - kRing + kRingSlack, so every position below that is
+// in HBM.  Sources lie below carry (db + span <= carry is required).
+// ---------------------------------------------------------------------------
+// Far ops are never forwarded (their sources lie below the window), so the
+// copy is issued before forwarding -- which then hands far-buffer sources on
+// to the ops that forward to them -- and only committed to LDS after it, so
+// the loads' latency hides under the forwarding rounds.
+struct FarCopy {
+    uint32_t v[4];          // this lane's buffer dwords 4l .. 4l+3
+    uint32_t used;          // buffer dwords filled (0: no far op in the window)
+};
+
+__device__ __forceinline__ FarCopy far_issue(FastLds& S, const Blk& k, uint32_t l,
+                                             uint32_t nwin, uint32_t carry, uint32_t o,
+                                             uint32_t L, uint32_t dp, uint32_t& db)
+{
+    FarCopy fc;
+    fc.used = 0;
+    const uint32_t span = dp ? dp : L;
+    // some byte may read below the ring: sp + kRing < step_end + 4 with
+    // step_end <= x + 259 and sp - db <= x - o (p == 0) or < p
+    const bool far = l < nwin && !(db & kLitFlag) && db + span <= carry &&
+                     db + kRing < o + (dp ? L : 0u) + 260u;
+    if (!wave_ballot(far))
+        return fc;
+    const uint32_t nd = far ? ((db + span + 3u) >> 2) - (db >> 2) : 0u;
+    const uint32_t incl0 = wave_incl_scan(nd);
+    const uint32_t acc_nd = incl0 <= kFarDw ? nd : 0u;     // the buffer takes a prefix of them
+    const uint32_t cum = wave_incl_scan(acc_nd);
+    const uint32_t used = lane_read(cum, kWave - 1);
+    fc.used = used;
+    const uint32_t gl_end = carry + kRingSlack - kRing;     // below: in HBM (may wrap: none)
+    const bool gl_any = carry + kRingSlack > kRing;
+    // Buffer dword t -> its op, as in the gather steps: flag each op's first
+    // buffer dword (S.flags, one byte per dword), scan the flag counts; the
+    // k-th op's (source dword - buffer dword) sits in a table at k (the
+    // window's op records are not written yet, so their space is free).
+    uint32_t* const delta = (uint32_t*)S.wop;
+    S.flags[l] = 0;
+    wave_order();
+    const uint64_t accm = wave_ballot(acc_nd != 0);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(accm >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)accm, 0u));
+    if (acc_nd) {
+        ((uint8_t*)S.flags)[cum - acc_nd] = 1;
+        delta[rank] = (db >> 2) - (cum - acc_nd);
+    }
+    wave_order();
+    const uint32_t f = S.flags[l];
+    const uint32_t nst = (uint32_t)__builtin_popcount(f);
+    const uint32_t jb = wave_incl_scan(nst) - nst - 1u;      // ops starting before 4l, minus 1
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        const uint32_t t = l * 4 + i;                        // buffer dword
+        const uint32_t j = (jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * i)) - 1u))) & 63u;
+        const uint32_t a = (t + delta[j]) * 4u;              // output byte offset, aligned
+        const bool need = t < used;
+        const bool hbm = need && gl_any && a + 4u <= gl_end;
+        fc.v[i] = S.ring[(a & kRingMask) >> 2];
+        if (hbm)
+            fc.v[i] = __builtin_nontemporal_load((gdword*)(k.out + a));
+    }
+    if (acc_nd)
+        db = kLitFlag | (kFarOff + 4u * (cum - acc_nd) + (db & 3u));
+    return fc;
+}
+
+__device__ __forceinline__ void far_commit(FastLds& S, uint32_t l, const FarCopy& fc)
+{
+    if (!fc.used)
+        return;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++)
+        if (l * 4 + i < fc.used)
+            S.far[l * 4 + i] = fc.v[i];
+}
+
+// ---------------------------------------------------------------------------
 template <bool STAMPS>
 __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
@@ -740,15 +839,21 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             }
             // ---- op descriptors: byte x of op j reads
             //   src[b + ((x - o) mod p)]   (p == 0: src[b + x - o])
-            // in the input (kLitFlag set in b) or in the output.  A match
-            // starts as b = o - d, p = d if it overlaps itself (d < L).
-            uint32_t db = lit ? Sv : o - Sv;
+            // in LDS at linear address b (kLitFlag set: the input staging or
+            // the far buffer; past the staging, the input in HBM) or in the
+            // output (ring / HBM).  A match starts as b = o - d, p = d if it
+            // overlaps itself (d < L).
+            uint32_t db = lit ? Sv + (kStageOff - k.P) : o - Sv;
             uint32_t dp = (!lit && Sv < L) ? Sv : 0u;
             // Source forwarding: a match whose source span lies inside one
             // earlier op of this window reads that op's source instead, so it
             // no longer waits for it.  Three parallel rounds reach the
             // sequential fixed point on ITB streams (600 -> 205 batches per
             // 64 KiB block).
+            FarCopy fc;
+            fc.used = 0;
+            if (kFarDw)
+                fc = far_issue(S, k, l, nwin, carry, o, L, dp, db);
             const uint32_t o_first = lane_read(o, 0);
             for (int round = 0; round < 3; round++) {
                 const uint32_t span = dp ? dp : L;
@@ -778,6 +883,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             }
             // end of each output-sourced op's source span: a batch may not read
             // its own output
+            if (kFarDw)
+                far_commit(S, l, fc);
             const bool outsrc = l < nwin && !(db & kLitFlag);
             const uint32_t send = outsrc ? db + (dp ? dp : L) : 0u;
             S.wop[l] = make_uint4(o, db, dp, dp ? 0xFFFFFFFFu / dp : 0u);   // mod by mulhi
@@ -830,6 +937,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         // Every byte the same way, branch-free: its op record (one
                         // 16-byte LDS read), then its source byte (one LDS read).
                         const uint8_t* lds = (const uint8_t*)&S;
+                        const uint32_t lin_end = kStageOff + k.staged;
+                        const uint32_t lin_in = kStageOff - k.P;    // LDS address - input position
                         uint4 op[4];
 #pragma unroll
                         for (uint32_t q = 0; q < 4; q++)
@@ -844,14 +953,13 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                             rr -= rr >= op[q].z ? op[q].z : 0u;  // (p == 0: rr = r)
                             const uint32_t sp = (op[q].y & ~kLitFlag) + rr;
                             const bool litq = (op[q].y & kLitFlag) != 0;
-                            const uint32_t rel = sp - k.P;
                             const bool old = xb < os;
                             const bool live = !old && xb < oe;
-                            const bool isg = live && (litq ? rel >= k.staged : sp + kRing < step_end + 4);
+                            const bool inlds = sp < lin_end;    // staging / far buffer
+                            const bool isg = live && (litq ? !inlds : sp + kRing < step_end + 4);
                             const uint32_t ring_a = kRingOff + ((old ? xb : sp) & kRingMask);
-                            const uint32_t stage_a = kStageOff + (rel < k.staged ? rel : 0u);
-                            addr[q] = (litq && !old) ? stage_a : ring_a;
-                            gsrc[q] = litq ? (sp | kLitFlag) : sp;
+                            addr[q] = (litq && !old) ? (inlds ? sp : 0u) : ring_a;
+                            gsrc[q] = litq ? ((sp - lin_in) | kLitFlag) : sp;
                             gmask |= isg ? (1u << q) : 0u;
                         }
                         uint32_t val = 0;
