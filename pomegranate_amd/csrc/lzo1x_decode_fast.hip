@@ -410,7 +410,8 @@ __device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
 // Diagnostic build only (STAMPS): per-phase s_memtime cycle sums go to
 // stamps[b * 8 + phase]; no output value depends on them.
 enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_WALKS,
-       PH_SPACE, PH_FLAGS, PH_GATHER, PH_NSTEP, PH_NBATCH, PH_NSLOW, PH_N };
+       PH_SPACE, PH_FLAGS, PH_GATHER, PH_NSTEP, PH_NBATCH, PH_NSLOW, PH_PWALK, PH_FAR, PH_N };
+static_assert(PH_N <= 16, "16 stamp slots per block");
 
 // Uniform walk of the true path from (pos, st) through lane i's segment
 // [c0, c1) until it lands on one of lane i's final-generation marks (then
@@ -716,29 +717,56 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         const uint32_t apos = shift_up1(xpos, entry_pos), ast = shift_up1(xst, entry_st);
         uint32_t fpos = apos, fst = ast;
         walk_uniform<true>(S, k, c0, c1, xgen, xpos, xst, fpos, fst);   // per lane (divergent)
-        uint32_t epos = 0, est = 0;
+        STAMP(PH_PWALK);
+        // The scan visits only the lanes that need it.  Where lane i's true
+        // entry E equals its assumed one, lanes i, i+1, ... stay right as long
+        // as each walk landed on the next lane's assumed entry (f_l == x_l)
+        // and none gave up, so the scan jumps to the first lane q where that
+        // fails: mm (lane q-1's walk missed lane q's assumed entry) or uk
+        // (lane q's own walk gave up), with E_q = f_{q-1}.
+        uint32_t epos = apos, est = ast;
         {
+            const uint64_t mm = wave_ballot(fpos != xpos || fst != xst) << 1;
+            const uint64_t uk = wave_ballot(fpos == kPosUnknown);
             uint32_t E = entry_pos, Est = entry_st;
-            for (uint32_t i = 0; i < (uint32_t)kWave; i++) {
+            uint32_t i = 0;
+            while (i < (uint32_t)kWave) {
+                if (E == lane_read(apos, i) && Est == lane_read(ast, i)) {
+                    const uint64_t from_i = ~0ull << i;
+                    const uint64_t cand = (mm & (from_i << 1)) | (uk & from_i);
+                    if (!cand) {                       // right through lane 63
+                        E = lane_read(fpos, kWave - 1);
+                        Est = lane_read(fst, kWave - 1);
+                        break;
+                    }
+                    const uint32_t q = (uint32_t)__builtin_ctzll(cand);
+                    if (q > i) {
+                        E = lane_read(fpos, q - 1);
+                        Est = lane_read(fst, q - 1);
+                        i = q;
+                    }
+                }
+                // lane i on its own, from its true entry E
                 if (l == i) {
                     epos = E;
                     est = Est;
                 }
                 const uint32_t ci1 = k.P + (i + 1) * kSeg;
-                if (E >= ci1)
-                    continue;                          // segment i has no true start
-                if (E == lane_read(apos, i) && Est == lane_read(ast, i) &&
-                    lane_read(fpos, i) != kPosUnknown) {
-                    E = lane_read(fpos, i);
-                    Est = lane_read(fst, i);
-                    continue;
+                if (E < ci1) {                         // else: segment i has no true start
+                    if (E == lane_read(apos, i) && Est == lane_read(ast, i) &&
+                        lane_read(fpos, i) != kPosUnknown) {
+                        E = lane_read(fpos, i);
+                        Est = lane_read(fst, i);
+                    } else {
+                        walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i),
+                                            lane_read(xpos, i), lane_read(xst, i), E, Est);
+                        if (STAMPS)
+                            acc[PH_WALKS] += 1;
+                    }
                 }
-                walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i), lane_read(xpos, i),
-                                    lane_read(xst, i), E, Est);
-                if (STAMPS)
-                    acc[PH_WALKS] += 1;
+                i++;
             }
-            fpos = E;                                  // (only lane 63's value is used)
+            fpos = E;                                  // (uniform: the piece's true exit)
             fst = Est;
         }
         const uint32_t next_pos = fpos, next_st = fst;
@@ -854,6 +882,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             fc.used = 0;
             if (kFarDw)
                 fc = far_issue(S, k, l, nwin, carry, o, L, dp, db);
+            STAMP(PH_FORM);
             const uint32_t o_first = lane_read(o, 0);
             for (int round = 0; round < 3; round++) {
                 const uint32_t span = dp ? dp : L;
@@ -885,6 +914,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             // its own output
             if (kFarDw)
                 far_commit(S, l, fc);
+            STAMP(PH_FAR);
             const bool outsrc = l < nwin && !(db & kLitFlag);
             const uint32_t send = outsrc ? db + (dp ? dp : L) : 0u;
             S.wop[l] = make_uint4(o, db, dp, dp ? 0xFFFFFFFFu / dp : 0u);   // mod by mulhi

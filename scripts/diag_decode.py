@@ -55,7 +55,7 @@ for stamp in (False, True):
           f"equal {torch.equal(out, src.arena)}")
 st = stamps.view(nb, 16).double().cpu().numpy()
 names = ["stage", "pass1", "merge", "count", "write", "form", "steps(write+publish)", "walks",
-         "space", "flags", "gather", "nstep", "nbatch", "nslow"]
-tot = st[:, [0,1,2,3,4,5,6,8,9,10]].sum(1)
+         "space", "flags", "gather", "nstep", "nbatch", "nslow", "pwalk", "fwd+far"]
+tot = st[:, [0,1,2,3,4,5,6,8,9,10,14,15]].sum(1)
 print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(names)}, "total", int(tot.mean()))
 print("zlen mean", float(zl.double().mean()))
