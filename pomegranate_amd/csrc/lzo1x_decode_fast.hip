@@ -87,11 +87,13 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t far[kFarDw];     // sources of this window's far matches (beyond the ring)
     uint32_t stage[kStageBytes / 4];
 
-    uint4 wop[kWave + 4];     // per window op: {o, source base (| kLitFlag), period, floor((2^32-1)/period)}
-    uint32_t flags[kWave];
+    uint4 wop[kWave];         // window op: {o, source base (| kLitFlag: LDS-linear), first chunk, L (| kLitFlag: needs HBM)}
+    uint2 wper[kWave];        // window op: {period, floor((2^32-1)/period)}
+    uint32_t flags[kWave];    // per-step chunk tags (far_issue: per-dword byte flags)
+    uint32_t sink;            // target of masked-off byte writes
     union {
         uint8_t marks[kPiece];        // parse: speculative path marks (pass 1, merge)
-        uint32_t opref[kOpMax];       // then: the piece's ops as instruction references
+        uint16_t opref[kOpMax];       // then: the piece's ops as instruction references
     };
     // decoder -> writer hand-off (LDS words, workgroup scope)
     uint32_t produced;      // output bytes final in the ring
@@ -105,6 +107,10 @@ constexpr uint32_t kStageOff = kRing + kFarBytes;                 // offsetof(Fa
 static_assert(offsetof(FastLds, ring) == kRingOff, "layout");
 static_assert(offsetof(FastLds, far) == kFarOff, "layout");
 static_assert(offsetof(FastLds, stage) == kStageOff, "layout");
+constexpr uint32_t kSinkOff = kStageOff + kStageBytes + (kWave * (16 + 8 + 4));   // offsetof(FastLds, sink)
+static_assert(offsetof(FastLds, sink) == kSinkOff, "layout");
+constexpr uint32_t kLdsMask = 0x3FFF;                              // LDS-linear address space
+static_assert(sizeof(FastLds) <= kLdsMask + 1, "linear LDS addresses are masked to 16 KiB");
 // 16 blocks per CU share its 160 KiB of LDS
 static_assert(sizeof(FastLds) * 2 * POM_WAVES_PER_EU <= 160 * 1024, "LDS budget");
 
@@ -407,11 +413,15 @@ __device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
 }
 
 
-// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums go to
-// stamps[b * 8 + phase]; no output value depends on them.
-enum { PH_STAGE, PH_PASS1, PH_MERGE, PH_COUNT, PH_WRITE, PH_FORM, PH_STEPS, PH_WALKS,
-       PH_SPACE, PH_FLAGS, PH_GATHER, PH_NSTEP, PH_NBATCH, PH_NSLOW, PH_PWALK, PH_FAR, PH_N };
-static_assert(PH_N <= 16, "16 stamp slots per block");
+// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums (slots
+// 0..CN_FIRST-1) and event counts (CN_*) go to stamps[b * kStampSlots + i];
+// no output value depends on them.  scripts/diag_decode.py knows this order.
+enum { PH_STAGE, PH_PASS1, PH_PWALK, PH_MERGE, PH_COUNT, PH_WRITE,
+       PH_WLOAD, PH_WSCAN, PH_FARI, PH_FWD, PH_FARC, PH_BATCH,
+       PH_SPACE, PH_FLAGS, PH_GATHER, PH_PUB,
+       CN_FIRST, CN_WALKS = CN_FIRST, CN_WINDOWS, CN_FARWIN, CN_BATCHES, CN_STEPS, PH_N };
+constexpr int kStampSlots = 32;
+static_assert(PH_N <= kStampSlots, "stamp slots per block");
 
 // Uniform walk of the true path from (pos, st) through lane i's segment
 // [c0, c1) until it lands on one of lane i's final-generation marks (then
@@ -612,6 +622,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         S.flushed = 0;
         S.state = 0;
     }
+    if (threadIdx.x < kWave)
+        S.flags[threadIdx.x] = 0;             // chunk tags start at 0x80000001
     __syncthreads();
     uint8_t* const out = dst + dst_off[b];
     if (wave == 1) {
@@ -645,6 +657,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     uint32_t entry_pos = 0, entry_st = ST_F;   // true entry of the current piece
     uint32_t carry = 0;                        // output produced so far
     uint32_t flushed_seen = 0;                 // last `flushed` read
+    uint32_t tag = 0;                          // step counter for the chunk tags
     bool done = false;                         // EOF consumed
 
     while (!refuse && !done) {
@@ -761,7 +774,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i),
                                             lane_read(xpos, i), lane_read(xst, i), E, Est);
                         if (STAMPS)
-                            acc[PH_WALKS] += 1;
+                            acc[CN_WALKS] += 1;
                     }
                 }
                 i++;
@@ -816,14 +829,14 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 if (r.eof)
                     break;
                 // An op is stored as a reference to its instruction
-                // (piece offset | state << 16 | part << 18, part 1 = trailing
-                // literals) and re-decoded when its window executes: 4 bytes
-                // of LDS instead of 8.
-                const uint32_t ref = (pos - k.P) | (st << 16);
+                // (piece offset | state << 10 | part << 12, part 1 = trailing
+                // literals; instructions start inside the 1-KiB piece) and is
+                // re-decoded when its window executes: 2 bytes of LDS, not 8.
+                const uint32_t ref = (pos - k.P) | (st << 10);
                 if (r.aL)
-                    S.opref[w++] = ref;
+                    S.opref[w++] = (uint16_t)ref;
                 if (r.bL)
-                    S.opref[w++] = ref | (1u << 18);
+                    S.opref[w++] = (uint16_t)(ref | (1u << 12));
                 pos = r.pos;
                 st = r.st;
             }
@@ -847,11 +860,14 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             uint32_t L = 0, Sv = 0;
             if (l < nwin) {
                 const uint32_t ref = S.opref[w0 + l];
-                const Step r = decode_step(S, k, k.P + (ref & 0xFFFFu), (ref >> 16) & 3u);
-                const bool part = (ref >> 18) != 0;
+                const Step r = decode_step(S, k, k.P + (ref & 0x3FFu), (ref >> 10) & 3u);
+                const bool part = (ref >> 12) != 0;
                 L = part ? r.bL : r.aL;
                 Sv = part ? r.bS : r.aS;
             }
+            STAMP(PH_WLOAD);
+            if (STAMPS)
+                acc[CN_WINDOWS] += 1;
             const uint32_t inc = wave_incl_scan(L);
             const uint32_t o = carry + inc - L;
             const uint32_t wtotal = lane_read(inc, kWave - 1);
@@ -878,11 +894,14 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             // no longer waits for it.  Three parallel rounds reach the
             // sequential fixed point on ITB streams (600 -> 205 batches per
             // 64 KiB block).
+            STAMP(PH_WSCAN);
             FarCopy fc;
             fc.used = 0;
             if (kFarDw)
                 fc = far_issue(S, k, l, nwin, carry, o, L, dp, db);
-            STAMP(PH_FORM);
+            STAMP(PH_FARI);
+            if (STAMPS && fc.used)
+                acc[CN_FARWIN] += 1;
             const uint32_t o_first = lane_read(o, 0);
             for (int round = 0; round < 3; round++) {
                 const uint32_t span = dp ? dp : L;
@@ -912,31 +931,77 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             }
             // end of each output-sourced op's source span: a batch may not read
             // its own output
+            STAMP(PH_FWD);
             if (kFarDw)
                 far_commit(S, l, fc);
-            STAMP(PH_FAR);
             const bool outsrc = l < nwin && !(db & kLitFlag);
-            const uint32_t send = outsrc ? db + (dp ? dp : L) : 0u;
-            S.wop[l] = make_uint4(o, db, dp, dp ? 0xFFFFFFFFu / dp : 0u);   // mod by mulhi
+            const uint32_t span = dp ? dp : L;
+            const uint32_t send = outsrc ? db + span : 0u;
+            uint32_t inv = 0;                          // mod by mulhi; only overlapping matches
+            if (wave_ballot(dp != 0))
+                inv = dp ? 0xFFFFFFFFu / dp : 0u;
+            // An op needs HBM reads if its literal source runs past the staging,
+            // or its output source may leave the ring before its last step
+            // (sp + kRing < step start + 260 for some byte; far ops the buffer
+            // did not take).
+            const uint32_t lin_end = kStageOff + k.staged;
+            const bool gop = l < nwin && (outsrc ? db + kRing < o + (dp ? L : 0u) + 260u
+                                                 : (db & ~kLitFlag) + span > lin_end);
+            // Chunks: op j covers output chunks cs .. cs + ceil(L/4) - 1 of the
+            // window, each up to 4 bytes of that op alone.
+            const uint32_t nch = l < nwin ? (L + 3u) >> 2 : 0u;
+            const uint32_t cinc = wave_incl_scan(nch);
+            const uint32_t cs = cinc - nch;
+            const uint32_t wchunks = lane_read(cinc, kWave - 1);
+            S.wop[l] = make_uint4(o, db, cs, L | (gop ? kLitFlag : 0u));
+            S.wper[l] = make_uint2(dp, inv);
             wave_order();
+            STAMP(PH_FARC);
             uint32_t s = 0;
             while (s < nwin) {
                 const uint32_t os = lane_read(o, s);
                 const bool brk = l > s && outsrc && send > os;
                 const uint64_t bm = wave_ballot(brk);
                 const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nwin;
-                const uint32_t oe = e < nwin ? lane_read(o, e) : carry + wtotal;
-                STAMP(PH_FORM);
+                const uint32_t c_beg = lane_read(cs, s);
+                const uint32_t c_end = e < nwin ? lane_read(cs, e) : wchunks;
+                const bool gbatch = wave_ballot(l >= s && l < e && gop) != 0;
+                const bool starter = l >= s && l < e;
+                STAMP(PH_BATCH);
                 if (STAMPS)
-                    acc[PH_NBATCH] += 1;
-                // ---- batch [s, e): output [os, oe), 64 dwords per step -------
-                const uint32_t base = os & ~3u;
-                uint32_t jcarry = s;                    // first op starting at/after the step
-                for (uint32_t xs = base; xs < oe; xs += 4 * kWave) {
-                    const uint32_t step_end = xs + 4 * kWave;
-                    // ring space: positions [step_end - kRing, xs) must be flushed
-                    // before this step overwrites their slots (and far reads
-                    // below need flushed >= step_end - kRing + kRingSlack).
+                    acc[CN_BATCHES] += 1;
+                // ---- batch [s, e): chunks [c_beg, c_end), 64 per step --------
+                uint32_t jcarry = s;                   // ops of the batch started before C
+                for (uint32_t C = c_beg; C < c_end; C += kWave) {
+                    // chunk -> op: each op starting in this step tags its first
+                    // chunk's slot; lane l's op is the last one started at or
+                    // before chunk C + l (a ballot and mbcnt, no scan).
+                    tag++;
+                    const uint32_t tagv = tag | 0x80000000u;   // far_issue's byte flags never set bit 31
+                    if (starter && cs >= C && cs < C + kWave)
+                        S.flags[cs - C] = tagv;
+                    wave_order();
+                    const bool st0 = S.flags[l] == tagv;
+                    const uint64_t M = wave_ballot(st0);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+                    const uint32_t j = (jcarry + below + (st0 ? 0u : ~0u)) & 63u;
+                    jcarry += (uint32_t)__builtin_popcountll(M);
+                    const uint4 op = S.wop[j];
+                    const uint2 pr = S.wper[j];
+                    const uint32_t c = C + l;
+                    const bool live = c < c_end;
+                    const uint32_t k4 = (c - op.z) * 4u;
+                    const uint32_t x = op.x + k4;
+                    const uint32_t Lj = op.w & ~kLitFlag;
+                    const uint32_t rem = Lj - k4;
+                    const uint32_t len = live ? (rem < 4u ? rem : 4u) : 0u;
+                    const uint32_t nl = c_end - C < (uint32_t)kWave ? c_end - C : (uint32_t)kWave;
+                    const uint32_t xs = lane_read(x, 0);
+                    const uint32_t step_end = lane_read(x + len, nl - 1);
+                    STAMP(PH_FLAGS);
+                    // ring space: the slots of [xs, step_end) must be flushed
+                    // (and HBM reads below need flushed >= step_end - kRing + kRingSlack).
                     for (uint32_t spin = 0; step_end > flushed_seen + kRing - kRingSlack; spin++) {
                         if (spin > (1u << 22)) {       // writer stuck: let the exact path redo it
                             refuse = true;
@@ -949,76 +1014,57 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         break;
                     STAMP(PH_SPACE);
                     if (STAMPS)
-                        acc[PH_NSTEP] += 1;
-                    // flag op starts per byte, count them per unit
-                    S.flags[l] = 0;
-                    wave_order();
-                    if (l >= s && l < e && o >= xs && o < step_end)
-                        ((uint8_t*)S.flags)[o - xs] = 1;
-                    wave_order();
-                    const uint32_t f = S.flags[l];
-                    const uint32_t nst = (uint32_t)__builtin_popcount(f);
-                    const uint32_t sincl = wave_incl_scan(nst);
-                    const uint32_t jb = jcarry + sincl - nst - 1;   // op before this unit's starts
-                    jcarry += lane_read(sincl, kWave - 1);
-                    STAMP(PH_FLAGS);
-                    const uint32_t x = xs + 4 * l;
+                        acc[CN_STEPS] += 1;
                     {
-                        // Every byte the same way, branch-free: its op record (one
-                        // 16-byte LDS read), then its source byte (one LDS read).
+                        // source offsets r_i = (k4 + i) mod p (p == 0: k4 + i)
+                        const uint32_t p = pr.x;
+                        uint32_t r[4];
+                        r[0] = k4 - p * (uint32_t)__umulhi(k4, pr.y);
+                        r[0] = min(r[0], r[0] - p);
+#pragma unroll
+                        for (uint32_t i = 1; i < 4; i++)
+                            r[i] = min(r[i - 1] + 1u, r[i - 1] + 1u - p);
+                        const bool lin = (op.y & kLitFlag) != 0;
+                        const uint32_t bb = live ? op.y & ~kLitFlag : 0u;
+                        // (linear sources past the staging read HBM below; masking
+                        // keeps their LDS read inside the allocation)
+                        const uint32_t amask = !live ? 0u : lin ? kLdsMask : kRingMask;
                         const uint8_t* lds = (const uint8_t*)&S;
-                        const uint32_t lin_end = kStageOff + k.staged;
-                        const uint32_t lin_in = kStageOff - k.P;    // LDS address - input position
-                        uint4 op[4];
-#pragma unroll
-                        for (uint32_t q = 0; q < 4; q++)
-                            op[q] = S.wop[jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * q)) - 1u))];
-                        uint32_t addr[4], gsrc[4];
-                        uint32_t gmask = 0;                     // bytes needing global reads
-#pragma unroll
-                        for (uint32_t q = 0; q < 4; q++) {
-                            const uint32_t xb = x + q;
-                            const uint32_t r = xb - op[q].x;
-                            uint32_t rr = r - op[q].z * (uint32_t)__umulhi(r, op[q].w);  // r mod p
-                            rr -= rr >= op[q].z ? op[q].z : 0u;  // (p == 0: rr = r)
-                            const uint32_t sp = (op[q].y & ~kLitFlag) + rr;
-                            const bool litq = (op[q].y & kLitFlag) != 0;
-                            const bool old = xb < os;
-                            const bool live = !old && xb < oe;
-                            const bool inlds = sp < lin_end;    // staging / far buffer
-                            const bool isg = live && (litq ? !inlds : sp + kRing < step_end + 4);
-                            const uint32_t ring_a = kRingOff + ((old ? xb : sp) & kRingMask);
-                            addr[q] = (litq && !old) ? (inlds ? sp : 0u) : ring_a;
-                            gsrc[q] = litq ? ((sp - lin_in) | kLitFlag) : sp;
-                            gmask |= isg ? (1u << q) : 0u;
-                        }
                         uint32_t val = 0;
 #pragma unroll
-                        for (uint32_t q = 0; q < 4; q++) {
-                            const uint32_t keep = x + q < oe ? 0xFFu : 0u;
-                            val |= ((uint32_t)lds[addr[q]] & keep) << (8 * q);
-                        }
-#ifdef POM_NOFAR_TIMING_ONLY
-                        gmask = 0;                              // timing experiment: wrong output
-#endif
-                        if (wave_ballot(gmask != 0)) {          // literal past staging / far match
-                            for (uint32_t q = 0; q < 4; q++) {
-                                if (!(gmask & (1u << q)))
-                                    continue;
-                                const uint32_t g = gsrc[q];
-                                const uint32_t bv = (g & kLitFlag)
-                                    ? (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + (g & ~kLitFlag)))
-                                    : global_byte_nt(k.out + g);
-                                val = (val & ~(0xFFu << (8 * q))) | (bv << (8 * q));
+                        for (uint32_t i = 0; i < 4; i++)
+                            val |= (uint32_t)lds[(bb + r[i]) & amask] << (8 * i);
+                        if (gbatch) {                          // literal past staging / far match
+                            const bool gj = (op.w & kLitFlag) != 0;
+                            uint32_t gmask = 0;
+#pragma unroll
+                            for (uint32_t i = 0; i < 4; i++) {
+                                const uint32_t sp = bb + r[i];
+                                const bool isg = gj && i < len && (lin ? sp >= lin_end : sp + kRing < xs + 260u);
+                                gmask |= isg ? (1u << i) : 0u;
+                            }
+                            if (wave_ballot(gmask != 0)) {
+                                const uint32_t lin_in = kStageOff - k.P;     // LDS address - input position
+                                for (uint32_t i = 0; i < 4; i++) {
+                                    if (!(gmask & (1u << i)))
+                                        continue;
+                                    const uint32_t sp = bb + r[i];
+                                    const uint32_t bv = lin
+                                        ? (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + (sp - lin_in)))
+                                        : global_byte_nt(k.out + sp);
+                                    val = (val & ~(0xFFu << (8 * i))) | (bv << (8 * i));
+                                }
                             }
                         }
-                        S.ring[(x & kRingMask) >> 2] = val;
+                        uint8_t* ldsw = (uint8_t*)&S;
+#pragma unroll
+                        for (uint32_t i = 0; i < 4; i++)
+                            ldsw[i < len ? ((x + i) & kRingMask) : kSinkOff + i] = (uint8_t)(val >> (8 * i));
                     }
                     wave_order();
                     STAMP(PH_GATHER);
-                    // bytes below min(step_end, oe) are final: hand them over
-                    lds_store(&S.produced, step_end < oe ? step_end : oe);
-                    STAMP(PH_STEPS);
+                    lds_store(&S.produced, step_end);  // bytes below are final: hand them over
+                    STAMP(PH_PUB);
                 }
                 if (refuse)
                     break;
@@ -1032,7 +1078,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
 
     if (STAMPS && l == 0)
         for (int i = 0; i < PH_N; i++)
-            stamps[(size_t)b * 16 + i] = acc[i];
+            stamps[(size_t)b * kStampSlots + i] = acc[i];
 #undef STAMP
     if (l == 0) {
         if (refuse) {
@@ -1066,7 +1112,7 @@ extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint6
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// Diagnostic: the same decoder with per-phase cycle stamps (8 x u64 per block).
+// Diagnostic: the same decoder with per-phase cycle stamps (kStampSlots x u64 per block).
 extern "C" int lzo_mi355x_debug_decompress_fast_stamps(
     const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint8_t* dst,
     const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* out_len, int32_t* status,

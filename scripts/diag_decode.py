@@ -32,7 +32,8 @@ zsrc = lzo.DeviceBatch(za, zb.off, zl)
 out = torch.zeros_like(src.arena); ob = lzo.DeviceBatch(out, src.off, src.length)
 ol = torch.zeros_like(zl); os_ = torch.zeros_like(zl)
 fb = torch.zeros(nb + 1, dtype=torch.int32, device=dev)
-stamps = torch.zeros(nb * 16, dtype=torch.int64, device=dev)
+SLOTS = 32
+stamps = torch.zeros(nb * SLOTS, dtype=torch.int64, device=dev)
 fn = lib.lzo_mi355x_debug_decompress_fast_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
@@ -53,9 +54,15 @@ for stamp in (False, True):
     e0.record(); run(stamp); e1.record(); torch.cuda.synchronize()
     print(f"stamps={stamp}: kernel {e0.elapsed_time(e1):.3f} ms, fallback {int(fb[0].item())}, "
           f"equal {torch.equal(out, src.arena)}")
-st = stamps.view(nb, 16).double().cpu().numpy()
-names = ["stage", "pass1", "merge", "count", "write", "form", "steps(write+publish)", "walks",
-         "space", "flags", "gather", "nstep", "nbatch", "nslow", "pwalk", "fwd+far"]
-tot = st[:, [0,1,2,3,4,5,6,8,9,10,14,15]].sum(1)
-print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(names)}, "total", int(tot.mean()))
+st = stamps.view(nb, SLOTS).double().cpu().numpy()
+# order of the kernel's PH_* / CN_* enum (lzo1x_decode_fast.hip)
+phases = ["stage", "pass1", "pwalk", "merge", "count", "write",
+          "wload", "wscan", "far_issue", "fwd", "far_commit+wop", "batch",
+          "space", "flags", "gather", "publish"]
+counts = ["walks", "windows", "far_windows", "batches", "steps"]
+tot = st[:, :len(phases)].sum(1)
+print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases)},
+      "total", int(tot.mean()))
+print("counts/block (mean):", {n: round(float(st[:, len(phases) + i].mean()), 1)
+                               for i, n in enumerate(counts)})
 print("zlen mean", float(zl.double().mean()))

@@ -1,0 +1,26 @@
+#!/bin/bash
+# SQ instruction-mix counters for the decode kernel, one rocprofv3 pass per
+# counter group (run on the GPU box).  Output: gpurun_out/sq_<tag>/.
+set -u
+TAG=${1:-cur}
+OUT=gpurun_out/sq_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || exit 1
+i=0
+for grp in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SALU SQ_BUSY_CYCLES" \
+           "SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH"; do
+  i=$((i+1))
+  timeout -k 10 200 rocprofv3 --pmc $grp --kernel-include-regex decode_fast -d $OUT/p$i -o sq --output-format csv -- python3 scripts/run_decode.py --reps 3 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python - "$OUT" <<'PY'
+import csv, collections, glob, sys
+d = collections.defaultdict(list)
+for f in glob.glob(sys.argv[1] + "/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "decode_fast" in r["Kernel_Name"]:
+            d[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, v in sorted(d.items()):
+    print(f"{k:24s} {sum(v)/len(v):16.0f}")
+PY
