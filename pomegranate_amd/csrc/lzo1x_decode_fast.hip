@@ -53,7 +53,10 @@ constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
 constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
 #ifndef POM_WRITER_SLEEP
-#define POM_WRITER_SLEEP 40                      // ~1.5K cycles between writer polls
+#define POM_WRITER_SLEEP 127                     // idle writer sleeps ~8K cycles between polls
+#endif
+#ifndef POM_FWD_ROUNDS
+#define POM_FWD_ROUNDS 3                         // source-forwarding rounds per window
 #endif
 #ifndef POM_WAVES_PER_EU
 #define POM_WAVES_PER_EU 8                       // 16 blocks (decoder + writer wave) per CU
@@ -131,6 +134,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
     const uint32_t row = lane_id() >> 4;
     v += (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
     return v;
+}
+
+// (diagnostics only) maximum over the wave
+__device__ __forceinline__ uint32_t wave_max_dbg(uint32_t v)
+{
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < (uint32_t)kWave; i++) {
+        const uint32_t x = __builtin_amdgcn_readlane(v, i);
+        m = x > m ? x : m;
+    }
+    return m;
 }
 
 __device__ __forceinline__ uint32_t shift_up1(uint32_t v, uint32_t fill)
@@ -419,7 +433,8 @@ __device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
 enum { PH_STAGE, PH_PASS1, PH_PWALK, PH_MERGE, PH_COUNT, PH_WRITE,
        PH_WLOAD, PH_WSCAN, PH_FARI, PH_FWD, PH_FARC, PH_BATCH,
        PH_SPACE, PH_FLAGS, PH_GATHER, PH_PUB,
-       CN_FIRST, CN_WALKS = CN_FIRST, CN_WINDOWS, CN_FARWIN, CN_BATCHES, CN_STEPS, PH_N };
+       CN_FIRST, CN_WALKS = CN_FIRST, CN_WINDOWS, CN_FARWIN, CN_BATCHES, CN_STEPS,
+       CN_IT_PASS1, CN_IT_PWALK, CN_IT_WALK, CN_IT_COUNT, CN_IT_WRITE, CN_FWD_ROUNDS, PH_N };
 constexpr int kStampSlots = 32;
 static_assert(PH_N <= kStampSlots, "stamp slots per block");
 
@@ -429,36 +444,39 @@ static_assert(PH_N <= kStampSlots, "stamp slots per block");
 // SPEC: per-lane speculative walk that gives up (pos = kPosUnknown) where the
 // exact slow decoder would be needed; the scalar scan then walks exactly.
 template <bool SPEC>
-__device__ __forceinline__ void walk_uniform(const FastLds& S, const Blk& k, uint32_t c0,
-                                             uint32_t c1, uint32_t gen, uint32_t xpos,
-                                             uint32_t xst, uint32_t& pos, uint32_t& st)
+__device__ __forceinline__ uint32_t walk_uniform(const FastLds& S, const Blk& k, uint32_t c0,
+                                                 uint32_t c1, uint32_t gen, uint32_t xpos,
+                                                 uint32_t xst, uint32_t& pos, uint32_t& st)
 {
+    uint32_t steps = 0;                      // (diagnostics)
     while (pos < c1) {
+        steps++;
         if (pos >= k.z) {
             pos = kPosEnd;
             st = 0;
-            return;
+            return steps;
         }
         if (pos >= c0 && S.marks[pos - k.P] == ((st + 1) | (gen << 2))) {
             pos = xpos;
             st = xst;
-            return;
+            return steps;
         }
         bool slow = false;
         const Step r = decode_step<SPEC>(S, k, pos, st, &slow);
         if (SPEC && slow) {
             pos = kPosUnknown;
             st = 0;
-            return;
+            return steps;
         }
         if (r.bad || r.eof) {
             pos = kPosEnd;
             st = 0;
-            return;
+            return steps;
         }
         pos = r.pos;
         st = r.st;
     }
+    return steps;
 }
 
 // ---------------------------------------------------------------------------
@@ -509,7 +527,10 @@ __device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
         if (state == 1)
             return;
         // Poll rarely: the scalar unit is shared by every wave of the CU, and a
-        // tight poll loop costs the decoder waves their SALU issue slots.
+        // tight poll loop costs the decoder waves their SALU issue slots.  (The
+        // ring's 3 KiB of headroom covers ~8K cycles of decoder output; waking
+        // the writer with s_wakeup per ready chunk measured slower than
+        // letting it drain several chunks per poll.)
         __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
     }
 }
@@ -551,11 +572,14 @@ __device__ __forceinline__ FarCopy far_issue(FastLds& S, const Blk& k, uint32_t 
     if (!wave_ballot(far))
         return fc;
     const uint32_t nd = far ? ((db + span + 3u) >> 2) - (db >> 2) : 0u;
-    const uint32_t incl0 = wave_incl_scan(nd);
-    const uint32_t acc_nd = incl0 <= kFarDw ? nd : 0u;     // the buffer takes a prefix of them
-    const uint32_t cum = wave_incl_scan(acc_nd);
-    const uint32_t used = lane_read(cum, kWave - 1);
+    const uint32_t cum = wave_incl_scan(nd);
+    const bool acc = far && cum <= kFarDw;                  // the buffer takes a prefix of them
+    const uint32_t acc_nd = acc ? nd : 0u;
+    const uint64_t accm = wave_ballot(acc);
+    const uint32_t used = accm ? lane_read(cum, 63u - (uint32_t)__builtin_clzll(accm)) : 0u;
     fc.used = used;
+    if (!used)
+        return fc;
     const uint32_t gl_end = carry + kRingSlack - kRing;     // below: in HBM (may wrap: none)
     const bool gl_any = carry + kRingSlack > kRing;
     // Buffer dword t -> its op, as in the gather steps: flag each op's first
@@ -565,7 +589,6 @@ __device__ __forceinline__ FarCopy far_issue(FastLds& S, const Blk& k, uint32_t 
     uint32_t* const delta = (uint32_t*)S.wop;
     S.flags[l] = 0;
     wave_order();
-    const uint64_t accm = wave_ballot(acc_nd != 0);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(accm >> 32),
                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)accm, 0u));
     if (acc_nd) {
@@ -695,6 +718,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         // and only marks of the final generation lie on the path that really
         // reaches xpos (a restart breaks the chain).
         uint32_t xpos, xst, xgen = 0;
+        uint32_t it_local = 0;                         // (diagnostics)
         if (c1 <= entry_pos) {                         // no instruction starts here
             xpos = entry_pos;
             xst = entry_st;
@@ -705,6 +729,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             uint32_t st = pos == entry_pos ? entry_st : ST_A;
             uint32_t gen = 0;
             while (pos < c1 && pos < k.z) {
+                if (STAMPS)
+                    it_local++;
                 if (pos >= c0)
                     S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 2));
                 bool slow = false;
@@ -729,7 +755,13 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         // scalar scan that reuses it and walks only where the guess was wrong.
         const uint32_t apos = shift_up1(xpos, entry_pos), ast = shift_up1(xst, entry_st);
         uint32_t fpos = apos, fst = ast;
-        walk_uniform<true>(S, k, c0, c1, xgen, xpos, xst, fpos, fst);   // per lane (divergent)
+        if (STAMPS)
+            acc[CN_IT_PASS1] += wave_max_dbg(it_local);
+        {
+            const uint32_t ws = walk_uniform<true>(S, k, c0, c1, xgen, xpos, xst, fpos, fst);   // per lane (divergent)
+            if (STAMPS)
+                acc[CN_IT_PWALK] += wave_max_dbg(ws);
+        }
         STAMP(PH_PWALK);
         // The scan visits only the lanes that need it.  Where lane i's true
         // entry E equals its assumed one, lanes i, i+1, ... stay right as long
@@ -771,10 +803,12 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         E = lane_read(fpos, i);
                         Est = lane_read(fst, i);
                     } else {
-                        walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i),
-                                            lane_read(xpos, i), lane_read(xst, i), E, Est);
-                        if (STAMPS)
+                        const uint32_t ws = walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i),
+                                                                lane_read(xpos, i), lane_read(xst, i), E, Est);
+                        if (STAMPS) {
                             acc[CN_WALKS] += 1;
+                            acc[CN_IT_WALK] += ws;
+                        }
                     }
                 }
                 i++;
@@ -790,7 +824,9 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         bool lane_eof = false, lane_err = false;
         {
             uint32_t pos = epos, st = est;
+            uint32_t itc = 0;
             while (pos < c1) {
+                itc++;
                 const Step r = decode_step(S, k, pos, st);
                 if (r.bad) {
                     lane_err = true;
@@ -808,6 +844,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 pos = r.pos;
                 st = r.st;
             }
+            if (STAMPS)
+                acc[CN_IT_COUNT] += wave_max_dbg(itc);
         }
         if (wave_ballot(lane_err)) {
             refuse = true;
@@ -824,7 +862,9 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         {
             uint32_t w = incl - nops;
             uint32_t pos = epos, st = est;
+            uint32_t itw = 0;
             while (pos < c1) {
+                itw++;
                 const Step r = decode_step(S, k, pos, st);
                 if (r.eof)
                     break;
@@ -840,6 +880,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 pos = r.pos;
                 st = r.st;
             }
+            if (STAMPS)
+                acc[CN_IT_WRITE] += wave_max_dbg(itw);
         }
         wave_order();
         STAMP(PH_WRITE);
@@ -903,11 +945,13 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             if (STAMPS && fc.used)
                 acc[CN_FARWIN] += 1;
             const uint32_t o_first = lane_read(o, 0);
-            for (int round = 0; round < 3; round++) {
+            for (int round = 0; round < POM_FWD_ROUNDS; round++) {
                 const uint32_t span = dp ? dp : L;
                 const bool need = l < nwin && !(db & kLitFlag) && db + span > o_first;
                 if (!wave_ballot(need))
                     break;
+                if (STAMPS)
+                    acc[CN_FWD_ROUNDS] += 1;
                 uint32_t k2 = 0;                       // last op with o <= db
 #pragma unroll
                 for (uint32_t w = 32; w >= 1; w >>= 1) {

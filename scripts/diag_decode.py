@@ -50,16 +50,20 @@ def run(stamp):
         fast(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), nb, sh)
 for stamp in (False, True):
     run(stamp); torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(); run(stamp); e1.record(); torch.cuda.synchronize()
-    print(f"stamps={stamp}: kernel {e0.elapsed_time(e1):.3f} ms, fallback {int(fb[0].item())}, "
-          f"equal {torch.equal(out, src.arena)}")
+    ts = []
+    for _ in range(1 if stamp else 10):
+        e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(); run(stamp); e1.record(); torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    print(f"stamps={stamp}: kernel {float(np.median(ts)):.3f} ms (median of {len(ts)}, min {min(ts):.3f}), "
+          f"fallback {int(fb[0].item())}, equal {torch.equal(out, src.arena)}")
 st = stamps.view(nb, SLOTS).double().cpu().numpy()
 # order of the kernel's PH_* / CN_* enum (lzo1x_decode_fast.hip)
 phases = ["stage", "pass1", "pwalk", "merge", "count", "write",
           "wload", "wscan", "far_issue", "fwd", "far_commit+wop", "batch",
           "space", "flags", "gather", "publish"]
-counts = ["walks", "windows", "far_windows", "batches", "steps"]
+counts = ["walks", "windows", "far_windows", "batches", "steps",
+          "it_pass1", "it_pwalk", "it_walk", "it_count", "it_write", "fwd_rounds"]
 tot = st[:, :len(phases)].sum(1)
 print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases)},
       "total", int(tot.mean()))
