@@ -1,0 +1,359 @@
+// lzo1x_encode_fast.hip -- the throughput LZO1X-1 encoder for MI355X (gfx950)
+// for blocks of up to 64 KiB (ITB-sized).  Output is byte-identical to
+// lib/minilzo.c:2922-3207 (lzo1x_1_compress) run with a zero-filled wrkmem;
+// the parse is SURVEY.md Appendix A.1.  Larger blocks are left with status
+// LZO_MI355X_ENC_PENDING for lzo1x_encode_kernel (lzo1x_kernels.hip).
+//
+// One workgroup per block, two waves:
+//
+//  * the PARSE wave walks the block 64 candidate positions at a time.  Every
+//    lane probes its own position against the dictionary as it was before the
+//    window (u16 positions in LDS, 0 = empty: the reference never stores
+//    position 0).  A lane's probe is exact as long as no earlier lane of the
+//    window that really probes writes a slot it reads; lanes set their two
+//    slots' bits in a claim bitmap with ds_or_rtn, and of any two lanes that
+//    share a slot at least one sees the other's bit, so cutting the window
+//    at the first lane that saw one keeps every lane before it exact (lane 0
+//    may be that lane -- the window then holds lane 0 alone).  Within
+//    the exact prefix the greedy parse proceeds as the reference does: the
+//    first matching lane emits a match, the lanes it covers are skipped (they
+//    neither probe nor update the dictionary), and the lane right after it
+//    continues -- several matches per window.  Candidate bytes and a 16-byte
+//    match compare come in one round trip per window; only matches of 16
+//    bytes or more need a wave-parallel extension.  The parse wave only emits
+//    tokens (literal run, match) into an LDS queue.
+//
+//  * the EMIT wave turns tokens into the LZO1X byte stream (lzo1x_emit.h) in
+//    an LDS ring and stores it to HBM, off the parse wave's critical path.
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "lzo_mi355x_kernels.h"
+#include "lzo1x_emit.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr uint32_t kSlots = emit::kSlots;
+constexpr uint32_t kMaxN = 65536;               // u16 dictionary positions (p < n - 13)
+constexpr uint32_t kTok = 128;                  // token queue entries
+constexpr uint32_t kStage = 2048;               // emitter output ring
+constexpr uint32_t kM2MaxOffset = 0x800;        // lib/minilzo.c M2_MAX_OFFSET
+constexpr uint32_t kM4MaxOffset = 0xBFFF;       // M4_MAX_OFFSET
+#ifndef POM_EMIT_SLEEP
+#define POM_EMIT_SLEEP 8
+#endif
+
+struct __attribute__((aligned(16))) EncLds {
+    uint16_t dict[kSlots];          // last probe position per hash slot (0 = empty)
+    uint32_t claim[kSlots / 32];    // per-window slot claims, cleared after each window
+    uint4 tok[kTok];                // {literal start, literal count, match length (0: tail), offset}
+    uint8_t stage[kStage];          // emitter output ring
+    uint32_t prod;                  // tokens published by the parse wave
+    uint32_t cons;                  // tokens consumed by the emit wave
+};
+// four blocks (eight waves) per CU
+static_assert(sizeof(EncLds) * 4 <= 160 * 1024, "LDS budget");
+
+__device__ __forceinline__ uint32_t lane_id() { return emit::lane(); }
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ void wave_order() { emit::order(); }
+
+__device__ __forceinline__ uint32_t lds_load(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+typedef __attribute__((address_space(1))) const uint32_t gdword;
+
+// NW little-endian dwords of the block starting at byte pos (any alignment).
+// Aligned dwords lying wholly past the block's last byte are not read (0):
+// callers cap every comparison at the block end.  Address-space-1 loads keep
+// these global_load (vmcnt), not flat_load.
+template <int NW>
+__device__ __forceinline__ void load_at(const uint8_t* in, uint32_t n, uint32_t pos, uint32_t (&w)[NW])
+{
+    const uintptr_t a = (uintptr_t)in + pos;
+    const uintptr_t a0 = a & ~(uintptr_t)3;
+    const uintptr_t last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
+    gdword* q = (gdword*)a0;
+    uint32_t r[NW + 1];
+#pragma unroll
+    for (int i = 0; i <= NW; i++)
+        r[i] = a0 + 4 * i <= last ? q[i] : 0u;
+    const uint32_t sh = (uint32_t)(a & 3);
+#pragma unroll
+    for (int i = 0; i < NW; i++)
+        w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+}
+
+// Index of the first differing byte of two 16-byte strings (16: none).
+__device__ __forceinline__ uint32_t first_diff16(const uint32_t (&a)[4], const uint32_t (&b)[4])
+{
+    uint32_t m = 16;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) {
+        const uint32_t x = a[i] ^ b[i];
+        m = x ? 4u * i + ((uint32_t)__builtin_ctz(x) >> 3) : m;
+    }
+    return m;
+}
+
+// Match length from index k0 on (the first k0 bytes match), wave-parallel,
+// 256 bytes per round trip, capped at the block end (lib/minilzo.c:3090-3102).
+__device__ uint32_t extend_match(const uint8_t* in, uint32_t n, uint32_t mc, uint32_t mp,
+                                 uint32_t k0, uint32_t l)
+{
+    const uint32_t lim = n - mp;
+    for (uint32_t k = k0;; k += 4 * kWave) {
+        const uint32_t idx = k + 4 * l;
+        uint32_t e = 0xFFFFFFFFu;
+        if (idx < lim) {
+            uint32_t a[1], b[1];
+            load_at<1>(in, n, mc + idx, a);
+            load_at<1>(in, n, mp + idx, b);
+            const uint32_t x = a[0] ^ b[0];
+            if (x)
+                e = idx + ((uint32_t)__builtin_ctz(x) >> 3);
+        }
+        if (idx + 4 > lim)
+            e = e < lim ? e : lim;
+        const uint64_t mis = wave_ballot(e != 0xFFFFFFFFu);
+        if (mis)
+            return lane_read(e, (uint32_t)__builtin_ctzll(mis));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Parse wave
+// ---------------------------------------------------------------------------
+__device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
+{
+    uint32_t tp = 0;                                // tokens produced
+    uint32_t cons_seen = 0;
+    auto push = [&](uint32_t from, uint32_t nlit, uint32_t mlen, uint32_t off) {
+        while (tp - cons_seen >= kTok) {             // the emit wave always drains
+            __builtin_amdgcn_s_sleep(2);
+            cons_seen = lds_load(&S.cons);
+        }
+        if (l == 0)
+            S.tok[tp % kTok] = make_uint4(from, nlit, mlen, off);
+        tp++;
+        lds_store(&S.prod, tp);
+    };
+
+    uint32_t ii = 0;                                // first byte not yet emitted
+    if (n > 13) {                                   // lib/minilzo.c:3167-3173
+        for (uint32_t s = l; s < kSlots / 2; s += kWave)
+            ((uint32_t*)S.dict)[s] = 0;             // zero-filled wrkmem: all EMPTY
+        for (uint32_t s = l; s < kSlots / 32; s += kWave)
+            S.claim[s] = 0;
+        wave_order();
+        const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
+        uint32_t ip = 4;
+        for (;;) {
+            const uint32_t p = ip + l;
+            const bool active = l == 0 || p < ip_end;   // the first probe always runs
+            uint32_t pw[4] = {0, 0, 0, 0};
+            uint32_t h1 = 0, h2 = 0, w1 = 0, w2 = 0;
+            if (active) {
+                load_at<4>(in, n, p, pw);
+                const uint32_t b0 = pw[0] & 0xFF, b1 = (pw[0] >> 8) & 0xFF;
+                const uint32_t b2 = (pw[0] >> 16) & 0xFF, b3 = pw[0] >> 24;
+                h1 = emit::slot_primary(b0, b1, b2, b3);
+                h2 = emit::slot_secondary(h1);
+                w1 = S.dict[h1];
+                w2 = S.dict[h2];
+            }
+            // claims: lane l sets its slots' bits; a bit already set means
+            // another lane of the window shares the slot
+            bool conflicted = false;
+            if (active) {
+                const uint32_t m1 = 1u << (h1 & 31), m2 = 1u << (h2 & 31);
+                const uint32_t o1 = atomicOr(&S.claim[h1 >> 5], m1);
+                const uint32_t o2 = atomicOr(&S.claim[h2 >> 5], m2);
+                conflicted = (o1 & m1) != 0 || (o2 & m2) != 0;
+            }
+            wave_order();
+            if (active) {
+                S.claim[h1 >> 5] = 0;
+                S.claim[h2 >> 5] = 0;
+            }
+            wave_order();
+            const uint64_t cm = wave_ballot(conflicted);
+            const uint64_t am = wave_ballot(active);
+            // (lane 0 can be the one that saw the bit -- its h2 is a later lane's
+            // h1 -- and is exact on its own: the window keeps at least lane 0)
+            uint32_t navail = cm ? (uint32_t)__builtin_ctzll(cm) : (uint32_t)__builtin_popcountll(am);
+            navail = navail ? navail : 1u;
+#ifdef POM_ENC_MAXLANES
+            navail = navail < POM_ENC_MAXLANES ? navail : POM_ENC_MAXLANES;   // (debugging)
+#endif
+
+            // Probe decision with the pre-window dictionary (exact for l < navail),
+            // lib/minilzo.c:2940-2971.
+            const bool v1 = l < navail && w1 != 0 && p - w1 <= kM4MaxOffset;
+            const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
+            uint32_t c1w[4] = {0, 0, 0, 0}, c2w[4] = {0, 0, 0, 0};
+            if (v1)
+                load_at<4>(in, n, w1, c1w);
+            if (v2)
+                load_at<4>(in, n, w2, c2w);
+            const uint32_t b3 = pw[0] >> 24;
+            bool tm = false;
+            uint32_t slot = h1, cand = w1;
+            uint32_t cw[4] = {c1w[0], c1w[1], c1w[2], c1w[3]};
+            if (v1) {
+                if (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3) {
+                    tm = true;
+                } else {
+                    slot = h2;
+                    if (v2 && (p - w2 <= kM2MaxOffset || (c2w[0] >> 24) == b3)) {
+                        tm = true;
+                        cand = w2;
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            cw[i] = c2w[i];
+                    }
+                }
+            }
+            // try_match (:2962-2971), then the match length as far as 16 bytes
+            const bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
+            uint32_t mlen = first_diff16(cw, pw);
+            mlen = mlen < n - p ? mlen : n - p;
+
+            // ---- greedy parse through the exact prefix [0, navail) ----------
+            const uint64_t okm = wave_ballot(ok);
+            uint64_t probed = navail >= 64 ? ~0ull : ((1ull << navail) - 1);
+            uint32_t r = 0;                          // next lane the parse reaches
+            bool done = false;
+            while (r < navail) {
+                const uint64_t rest = okm & (~0ull << r);
+                if (!rest)
+                    break;
+                const uint32_t q = (uint32_t)__builtin_ctzll(rest);
+                const uint32_t mp = ip + q;
+                const uint32_t mc = lane_read(cand, q);
+                uint32_t len = lane_read(mlen, q);
+                if (len == 16 && n - mp > 16)
+                    len = extend_match(in, n, mc, mp, 16, l);
+                push(ii, mp - ii, len, mp - mc);
+                ii = mp + len;
+                // lanes covered by the match neither probe nor update (:3051-3150)
+                const uint32_t cov_end = q + len < 64 ? q + len : 64;
+                if (cov_end > q + 1)
+                    probed &= ~((cov_end >= 64 ? ~0ull : ((1ull << cov_end) - 1)) & (~0ull << (q + 1)));
+                r = q + len;
+                if (ii >= ip_end) {                  // :3151-3152
+                    done = true;
+                    break;
+                }
+            }
+            // UPDATE_I of every lane that probed, in place: their slots are distinct
+            if ((probed >> l) & 1ull)
+                S.dict[slot] = (uint16_t)p;
+            wave_order();
+            if (done)
+                break;
+            ip += r > navail ? r : navail;
+            if (ip >= ip_end)
+                break;
+        }
+    }
+    push(ii, n - ii, 0, 0);                          // tail + EOF
+}
+
+// ---------------------------------------------------------------------------
+// Emit wave
+// ---------------------------------------------------------------------------
+__device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap,
+                          uint32_t* out_len, int32_t* status, uint32_t b)
+{
+    emit::Enc e;
+    e.in = in;
+    e.n = n;
+    e.out = out;
+    e.cap = cap;
+    e.stage = S.stage;
+    e.smask = kStage - 1;
+    e.sflush = kStage / 2;
+    e.op = e.flushed = 0;
+    uint32_t ct = 0;                                 // tokens consumed
+    for (;;) {
+        const uint32_t prod = lds_load(&S.prod);
+        if (ct == prod) {
+            __builtin_amdgcn_s_sleep(POM_EMIT_SLEEP);
+            continue;
+        }
+        while (ct < prod) {
+            const uint4 t = S.tok[ct % kTok];
+            ct++;
+            if (t.z == 0) {                          // tail literals + EOF: the block is done
+                emit::tail_and_eof(e, t.x);
+                if (lane_id() == 0) {
+                    out_len[b] = e.op;
+                    status[b] = e.op <= e.cap ? 0 : -5;    // LZO_E_OK / LZO_E_OUTPUT_OVERRUN
+                }
+                return;
+            }
+            if (t.y) {
+                emit::lit_header(e, t.y);
+                emit::lits(e, t.x, t.y);
+            }
+            emit::match(e, t.z, t.w);
+            emit::maybe_flush(e);
+            lds_store(&S.cons, ct);
+        }
+    }
+}
+
+__global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks)
+{
+    __shared__ EncLds S;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t n = src_len[b];
+    if (n > kMaxN) {                                 // positions must fit the u16 dictionary
+        if (threadIdx.x == 0)
+            status[b] = LZO_MI355X_ENC_PENDING;
+        return;
+    }
+    const uint32_t l = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x == 0) {
+        S.prod = 0;
+        S.cons = 0;
+    }
+    __syncthreads();
+    const uint8_t* in = src + src_off[b];
+    if (wave == 0)
+        parse_wave(S, in, n, l);
+    else
+        emit_wave(S, in, n, dst + dst_off[b], dst_cap[b], out_len, status, b);
+}
+
+}  // namespace
+
+extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_t* src_off,
+                                               const uint32_t* src_len, uint8_t* dst,
+                                               const uint64_t* dst_off, const uint32_t* dst_cap,
+                                               uint32_t* out_len, int32_t* status,
+                                               uint32_t nblocks, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_encode_fast_kernel, dim3(nblocks), dim3(2 * kWave), 0, stream, src,
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

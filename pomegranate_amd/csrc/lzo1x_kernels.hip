@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "lzo_mi355x_kernels.h"
+#include "lzo1x_emit.h"
 
 namespace {
 
@@ -369,165 +370,13 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
 // committed in position order with ds_max.
 //   dict word: [31:25] claiming lane (0x7F = none), [24:0] position+1 (0 = EMPTY)
 // ---------------------------------------------------------------------------
-constexpr uint32_t kSlots = 1u << 14;            // D_BITS 14, lib/minilzo.c:2627
+constexpr uint32_t kSlots = emit::kSlots;
 constexpr uint32_t kPosMask = (1u << 25) - 1;
 constexpr uint32_t kNoClaim = 0x7Fu << 25;
 constexpr uint32_t kStage = 8192;
-constexpr uint32_t kStageMask = kStage - 1;
-constexpr uint32_t kStageFlush = 4096;
-
-struct Enc {
-    const uint8_t* in;
-    uint32_t n;
-    uint8_t* out;
-    uint32_t cap;
-    uint8_t* stage;
-    uint32_t op, flushed;
-};
-
-__device__ __forceinline__ void enc_flush(Enc& e, uint32_t upto)
-{
-    wave_order();
-    const uint32_t l = lane_id();
-    for (uint32_t k = e.flushed; k < upto; k += kWave) {
-        const uint32_t j = k + l;
-        if (j < upto && j < e.cap)
-            e.out[j] = e.stage[j & kStageMask];
-    }
-    e.flushed = upto;
-    wave_order();
-}
-
-// Keep the last two bytes staged: a following short literal run ORs its
-// length into out[op-2] (lib/minilzo.c:3027-3030, 3181-3182).
-__device__ __forceinline__ void enc_maybe_flush(Enc& e)
-{
-    if (e.op - e.flushed >= kStageFlush + 2)
-        enc_flush(e, e.op - 2);
-}
-
-__device__ __forceinline__ void enc_byte(Enc& e, uint32_t v)
-{
-    if (lane_id() == 0)
-        e.stage[e.op & kStageMask] = (uint8_t)v;
-    wave_order();
-    e.op++;
-}
-
-__device__ __forceinline__ void enc_patch(Enc& e, uint32_t v)
-{
-    if (lane_id() == 0)
-        e.stage[(e.op - 2) & kStageMask] |= (uint8_t)v;
-    wave_order();
-}
-
-__device__ __forceinline__ void enc_zeros(Enc& e, uint32_t count)
-{
-    const uint32_t l = lane_id();
-    while (count > 0) {
-        const uint32_t c = count < (uint32_t)kWave ? count : (uint32_t)kWave;
-        if (l < c)
-            e.stage[(e.op + l) & kStageMask] = 0;
-        wave_order();
-        e.op += c;
-        count -= c;
-        enc_maybe_flush(e);
-    }
-}
-
-// ext(x): x/255 zero bytes then the remainder (lib/minilzo.c:3034-3046)
-__device__ __forceinline__ void enc_ext(Enc& e, uint32_t x)
-{
-    const uint32_t z = (x - 1) / 255;
-    enc_zeros(e, z);
-    enc_byte(e, x - 255 * z);
-}
-
-__device__ __forceinline__ void enc_lits(Enc& e, uint32_t from, uint32_t count)
-{
-    const uint32_t l = lane_id();
-    while (count > 0) {
-        const uint32_t c = count < (uint32_t)kWave ? count : (uint32_t)kWave;
-        if (l < c)
-            e.stage[(e.op + l) & kStageMask] = e.in[from + l];
-        wave_order();
-        e.op += c;
-        from += c;
-        count -= c;
-        enc_maybe_flush(e);
-    }
-}
-
-// Literal-run header (lib/minilzo.c:3023-3048, tail :3179-3199)
-__device__ __forceinline__ void enc_lit_header(Enc& e, uint32_t r)
-{
-    if (r <= 3)
-        enc_patch(e, r);
-    else if (r <= 18)
-        enc_byte(e, r - 3);
-    else {
-        enc_byte(e, 0);
-        enc_ext(e, r - 18);
-    }
-}
-
-// Match token (lib/minilzo.c:3064-3145)
-__device__ __forceinline__ void enc_match(Enc& e, uint32_t len, uint32_t off)
-{
-    if (len <= 8) {
-        if (off <= 0x800) {
-            const uint32_t o = off - 1;
-            enc_byte(e, ((len - 1) << 5) | ((o & 7) << 2));
-            enc_byte(e, o >> 3);
-            return;
-        }
-        if (off <= 0x4000) {
-            const uint32_t o = off - 1;
-            enc_byte(e, 0x20 | (len - 2));
-            enc_byte(e, (o & 63) << 2);
-            enc_byte(e, o >> 6);
-            return;
-        }
-        const uint32_t o = off - 0x4000;
-        enc_byte(e, 0x10 | ((o & 0x4000) >> 11) | (len - 2));
-        enc_byte(e, (o & 63) << 2);
-        enc_byte(e, o >> 6);
-        return;
-    }
-    uint32_t o;
-    if (off <= 0x4000) {
-        o = off - 1;
-        if (len <= 33)
-            enc_byte(e, 0x20 | (len - 2));
-        else {
-            enc_byte(e, 0x20);
-            enc_ext(e, len - 33);
-        }
-    } else {
-        o = off - 0x4000;
-        const uint32_t hi = (o & 0x4000) >> 11;
-        if (len <= 9)
-            enc_byte(e, 0x10 | hi | (len - 2));
-        else {
-            enc_byte(e, 0x10 | hi);
-            enc_ext(e, len - 9);
-        }
-    }
-    enc_byte(e, (o & 63) << 2);
-    enc_byte(e, o >> 6);
-}
-
-__device__ __forceinline__ uint32_t slot_primary(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t b3)
-{
-    uint32_t v = (((b3 << 6) ^ b2) << 5) ^ b1;     // DX3(p,5,5,6), lib/minilzo.c:2697-2704
-    v = (v << 5) ^ b0;
-    return ((v * 33u) >> 5) & (kSlots - 1);       // D_INDEX1, :2629
-}
-
-__device__ __forceinline__ uint32_t slot_secondary(uint32_t h)
-{
-    return (h & 0x7FFu) ^ 0x201Fu;                // D_INDEX2, :2630
-}
+using emit::Enc;
+using emit::slot_primary;
+using emit::slot_secondary;
 
 // Greedy parse over in[0, n), n > 13.  Returns the tail length (n - ii).
 __device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
@@ -614,8 +463,8 @@ __device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
         const uint32_t mc = lane_read(cand, q);
 
         if (mp > ii) {                             // pending literals
-            enc_lit_header(e, mp - ii);
-            enc_lits(e, ii, mp - ii);
+            emit::lit_header(e, mp - ii);
+            emit::lits(e, ii, mp - ii);
         }
         // Match length: first mismatch at index >= 3, capped at the block end
         // (lib/minilzo.c:3051-3102).
@@ -629,8 +478,8 @@ __device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
                 break;
             }
         }
-        enc_match(e, len, mp - mc);
-        enc_maybe_flush(e);
+        emit::match(e, len, mp - mc);
+        emit::maybe_flush(e);
         ip = mp + len;
         ii = ip;
         if (ip >= ip_end)
@@ -639,6 +488,9 @@ __device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
     return n - ii;
 }
 
+// PENDING_ONLY: runs after lzo1x_encode_fast_kernel and takes only the blocks
+// it left with status kEncPending (larger than 64 KiB).
+template <bool PENDING_ONLY>
 __global__ __launch_bounds__(kWave) void lzo1x_encode_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
@@ -650,6 +502,8 @@ __global__ __launch_bounds__(kWave) void lzo1x_encode_kernel(
     const uint32_t b = blockIdx.x;
     if (b >= nblocks)
         return;
+    if (PENDING_ONLY && status[b] != LZO_MI355X_ENC_PENDING)
+        return;
     const uint32_t l = lane_id();
     Enc e;
     e.in = src + src_off[b];
@@ -657,6 +511,8 @@ __global__ __launch_bounds__(kWave) void lzo1x_encode_kernel(
     e.out = dst + dst_off[b];
     e.cap = dst_cap[b];
     e.stage = stage;
+    e.smask = kStage - 1;
+    e.sflush = kStage / 2;
     e.op = e.flushed = 0;
     if (e.n > kPosMask - 1) {                      // positions must fit 25 bits
         if (l == 0) {
@@ -675,18 +531,7 @@ __global__ __launch_bounds__(kWave) void lzo1x_encode_kernel(
         wave_order();
         t = enc_parse(e, dict);
     }
-    if (t > 0) {                                   // tail, lib/minilzo.c:3175-3199
-        const uint32_t ii = e.n - t;
-        if (e.op == 0 && t <= 238)
-            enc_byte(e, 17 + t);
-        else
-            enc_lit_header(e, t);
-        enc_lits(e, ii, t);
-    }
-    enc_byte(e, 0x11);                             // EOF, lib/minilzo.c:3201-3203
-    enc_byte(e, 0);
-    enc_byte(e, 0);
-    enc_flush(e, e.op);
+    emit::tail_and_eof(e, e.n - t);                // lib/minilzo.c:3175-3203
     if (l == 0) {
         out_len[b] = e.op;
         status[b] = e.op <= e.cap ? E_OK : E_OUTPUT_OVERRUN;
@@ -702,12 +547,16 @@ extern "C" int lzo_mi355x_launch_compress(const uint8_t* src, const uint64_t* sr
                                           const uint32_t* src_len, uint8_t* dst,
                                           const uint64_t* dst_off, const uint32_t* dst_cap,
                                           uint32_t* out_len, int32_t* status,
-                                          uint32_t nblocks, hipStream_t stream)
+                                          uint32_t nblocks, int pending_only, hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_encode_kernel, dim3(nblocks), dim3(kWave), 0, stream, src, src_off,
-                       src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
+    if (pending_only)
+        hipLaunchKernelGGL(lzo1x_encode_kernel<true>, dim3(nblocks), dim3(kWave), 0, stream, src,
+                           src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
+    else
+        hipLaunchKernelGGL(lzo1x_encode_kernel<false>, dim3(nblocks), dim3(kWave), 0, stream, src,
+                           src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

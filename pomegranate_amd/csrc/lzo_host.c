@@ -146,8 +146,16 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                             uint32_t *out_len, int32_t *status, uint32_t nblocks,
                             void *stream)
 {
+    /* blocks up to 64 KiB: the throughput encoder; larger ones are left
+     * pending for the general encoder, whose other workgroups exit at once */
+    hipStream_t s = (hipStream_t)stream;
+    if (nblocks == 0)
+        return 0;
+    if (lzo_mi355x_launch_compress_fast(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
+                                        status, nblocks, s) != 0)
+        return -1;
     return lzo_mi355x_launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                      status, nblocks, (hipStream_t)stream);
+                                      status, nblocks, 1, s);
 }
 
 size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)

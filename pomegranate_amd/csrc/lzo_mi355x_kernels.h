@@ -10,11 +10,24 @@
 extern "C" {
 #endif
 
+/* status of a block lzo1x_encode_fast_kernel left to the general encoder */
+#define LZO_MI355X_ENC_PENDING 0x7FFF0002
+
+/* Throughput encoder (lzo1x_encode_fast.hip), blocks of up to 64 KiB; larger
+ * blocks get status LZO_MI355X_ENC_PENDING. */
+int lzo_mi355x_launch_compress_fast(const uint8_t *src, const uint64_t *src_off,
+                                    const uint32_t *src_len, uint8_t *dst,
+                                    const uint64_t *dst_off, const uint32_t *dst_cap,
+                                    uint32_t *out_len, int32_t *status, uint32_t nblocks,
+                                    hipStream_t stream);
+
+/* General encoder (lzo1x_kernels.hip), any block size below 32 MiB.
+ * pending_only: only blocks whose status is LZO_MI355X_ENC_PENDING. */
 int lzo_mi355x_launch_compress(const uint8_t *src, const uint64_t *src_off,
                                const uint32_t *src_len, uint8_t *dst,
                                const uint64_t *dst_off, const uint32_t *dst_cap,
                                uint32_t *out_len, int32_t *status, uint32_t nblocks,
-                               hipStream_t stream);
+                               int pending_only, hipStream_t stream);
 
 /* Exact (grammar-serial) decoder, lzo1x_decompress_safe semantics.  fb NULL:
  * grid entry b decodes block b (ngrid = nblocks).  Otherwise the fb[0] blocks
