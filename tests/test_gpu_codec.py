@@ -132,3 +132,47 @@ def test_host_batch_api(dev, edge, malformed):
     assert rc == 0
     assert st == malformed["rc"]
     assert outs == [o[:c] for o, c in zip(malformed["outs"], malformed["caps"])]
+
+
+def _adversarial_blocks():
+    """Inputs aimed at the throughput encoder's windowing
+    (lzo1x_encode_fast.hip): short periods (every lane of a window hashes to
+    the same few slots), periods around the 64-lane window, 4-byte patterns
+    that collide in the 16384-slot dictionary, long matches (the 16-byte
+    speculative compare and the wave-parallel extension), matches running
+    into the block end, sizes around the 64 KiB u16-position limit (65536
+    takes the fast kernel, 65537 the general one), and the 14..17-byte blocks
+    whose first probe lies at or past ip_end."""
+    rng = np.random.default_rng(11)
+    out = []
+    for period in (1, 2, 3, 4, 5, 7, 8, 13, 31, 32, 33, 63, 64, 65, 67, 127, 128, 129, 255):
+        unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+        out.append((unit * (4096 // period + 1))[:4096])
+    # many positions hashing alike: few distinct 4-byte words, shuffled
+    words = rng.integers(0, 2**32, 24, dtype=np.uint64).astype(np.uint32)
+    out.append(words[rng.integers(0, 24, 8192)].tobytes())
+    # random data with long repeats at assorted distances, some to the end
+    base = rng.integers(0, 256, 30000, dtype=np.uint8).tobytes()
+    mix = bytearray(base)
+    for k in range(40):
+        a = int(rng.integers(0, len(mix) - 600)); L = int(rng.integers(4, 600))
+        b = int(rng.integers(a + 1, len(mix) - L))
+        mix[b:b + L] = mix[a:a + L]
+    mix += mix[-5000:]
+    out.append(bytes(mix))
+    for n in (14, 15, 16, 17, 18, 29, 65535, 65536, 65537):
+        d = rng.integers(0, 4, n, dtype=np.uint8).tobytes()
+        out.append(d)
+    out.append(bytes(65536))                          # one long match to the end
+    out.append(bytes(70000))                          # the same past 64 KiB
+    return out
+
+
+def test_encoder_adversarial_vs_oracle(dev, gu, oracle):
+    blocks = _adversarial_blocks()
+    comps, st = gu.gpu_compress(torch, blocks, dev, shift=3)
+    assert all(s == 0 for s in st)
+    for i, (b, c) in enumerate(zip(blocks, comps)):
+        assert c == oracle.compress(b), (i, len(b))
+    outs, st2, _ = gu.gpu_decompress(torch, comps, [len(b) for b in blocks], dev, shift=1)
+    assert all(s == 0 for s in st2) and outs == blocks
