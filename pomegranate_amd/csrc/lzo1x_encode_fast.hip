@@ -171,34 +171,12 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
                 w1 = S.dict[h1];
                 w2 = S.dict[h2];
             }
-            // claims: lane l sets its slots' bits; a bit already set means
-            // another lane of the window shares the slot
-            bool conflicted = false;
-            if (active) {
-                const uint32_t m1 = 1u << (h1 & 31), m2 = 1u << (h2 & 31);
-                const uint32_t o1 = atomicOr(&S.claim[h1 >> 5], m1);
-                const uint32_t o2 = atomicOr(&S.claim[h2 >> 5], m2);
-                conflicted = (o1 & m1) != 0 || (o2 & m2) != 0;
-            }
-            wave_order();
-            if (active) {
-                S.claim[h1 >> 5] = 0;
-                S.claim[h2 >> 5] = 0;
-            }
-            wave_order();
-            const uint64_t cm = wave_ballot(conflicted);
             const uint64_t am = wave_ballot(active);
-            // (lane 0 can be the one that saw the bit -- its h2 is a later lane's
-            // h1 -- and is exact on its own: the window keeps at least lane 0)
-            uint32_t navail = cm ? (uint32_t)__builtin_ctzll(cm) : (uint32_t)__builtin_popcountll(am);
-            navail = navail ? navail : 1u;
-#ifdef POM_ENC_MAXLANES
-            navail = navail < POM_ENC_MAXLANES ? navail : POM_ENC_MAXLANES;   // (debugging)
-#endif
+            const uint32_t nact = (uint32_t)__builtin_popcountll(am);
 
-            // Probe decision with the pre-window dictionary (exact for l < navail),
-            // lib/minilzo.c:2940-2971.
-            const bool v1 = l < navail && w1 != 0 && p - w1 <= kM4MaxOffset;
+            // Probe decision of every active lane with the pre-window
+            // dictionary, lib/minilzo.c:2940-2971 (exact up to the cut below).
+            const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
             const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
             uint32_t c1w[4] = {0, 0, 0, 0}, c2w[4] = {0, 0, 0, 0};
             if (v1)
@@ -228,40 +206,88 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
             uint32_t mlen = first_diff16(cw, pw);
             mlen = mlen < n - p ? mlen : n - p;
 
-            // ---- greedy parse through the exact prefix [0, navail) ----------
+            // ---- the greedy path through the window, speculatively ----------
+            // From lane 0: a matching lane jumps over its match, any other
+            // lane is a literal.  Lanes inside matches neither probe nor
+            // update the dictionary (:3051-3150).
             const uint64_t okm = wave_ballot(ok);
-            uint64_t probed = navail >= 64 ? ~0ull : ((1ull << navail) - 1);
-            uint32_t r = 0;                          // next lane the parse reaches
-            bool done = false;
-            while (r < navail) {
-                const uint64_t rest = okm & (~0ull << r);
-                if (!rest)
+            uint64_t path = 0, mstart = 0;
+            uint32_t end = 0;                        // lane where the path leaves the window
+            while (end < nact) {
+                const uint64_t rest = okm & (~0ull << end);
+                const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
+                const uint32_t lit_end = q < nact ? q : nact;
+                if (lit_end > end)                   // literal lanes end .. lit_end-1
+                    path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
+                if (q >= nact) {
+                    end = nact;
                     break;
-                const uint32_t q = (uint32_t)__builtin_ctzll(rest);
-                const uint32_t mp = ip + q;
-                const uint32_t mc = lane_read(cand, q);
+                }
+                path |= 1ull << q;
+                mstart |= 1ull << q;
                 uint32_t len = lane_read(mlen, q);
-                if (len == 16 && n - mp > 16)
-                    len = extend_match(in, n, mc, mp, 16, l);
-                push(ii, mp - ii, len, mp - mc);
+                if (len == 16 && n - (ip + q) > 16) {
+                    len = extend_match(in, n, lane_read(cand, q), ip + q, 16, l);
+                    mlen = l == q ? len : mlen;
+                }
+                end = q + len;
+            }
+
+            // ---- exactness: claims among the path lanes only ------------------
+            // Path lane l reads its two slots and writes one of them.  Of two
+            // path lanes sharing a slot at least one sees the other's bit
+            // (same-address LDS atomics of a wave serialise), so every path
+            // lane before the first lane that saw one is exact; lane 0 always
+            // is.
+            const bool onpath = (path >> l) & 1ull;
+            bool conflicted = false;
+            if (onpath) {
+                const uint32_t m1 = 1u << (h1 & 31), m2 = 1u << (h2 & 31);
+                const uint32_t o1 = atomicOr(&S.claim[h1 >> 5], m1);
+                const uint32_t o2 = atomicOr(&S.claim[h2 >> 5], m2);
+                conflicted = (o1 & m1) != 0 || (o2 & m2) != 0;
+            }
+            wave_order();
+            if (onpath) {
+                S.claim[h1 >> 5] = 0;
+                S.claim[h2 >> 5] = 0;
+            }
+            wave_order();
+            const uint64_t cm = wave_ballot(conflicted);
+            uint32_t cut = cm ? (uint32_t)__builtin_ctzll(cm) : 0xFFFFFFFFu;
+            if (cut == 0) {                          // lane 0 alone: cut at its path successor
+                const uint64_t succ = path & ~1ull;
+                cut = succ ? (uint32_t)__builtin_ctzll(succ) : end;
+            }
+#ifdef POM_ENC_MAXLANES
+            cut = cut < POM_ENC_MAXLANES ? cut : POM_ENC_MAXLANES;   // (debugging: a path lane)
+            while (cut < 64 && !((path >> cut) & 1ull))
+                cut++;
+#endif
+            if (cut < end)                           // the window ends at a path lane
+                end = cut;
+            const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
+
+            // ---- tokens for the matches before the cut ------------------------
+            bool done = false;
+            for (uint64_t mm = mstart & keep; mm; mm &= mm - 1) {
+                const uint32_t q = (uint32_t)__builtin_ctzll(mm);
+                const uint32_t mp = ip + q;
+                const uint32_t len = lane_read(mlen, q);
+                push(ii, mp - ii, len, mp - lane_read(cand, q));
                 ii = mp + len;
-                // lanes covered by the match neither probe nor update (:3051-3150)
-                const uint32_t cov_end = q + len < 64 ? q + len : 64;
-                if (cov_end > q + 1)
-                    probed &= ~((cov_end >= 64 ? ~0ull : ((1ull << cov_end) - 1)) & (~0ull << (q + 1)));
-                r = q + len;
                 if (ii >= ip_end) {                  // :3151-3152
                     done = true;
                     break;
                 }
             }
-            // UPDATE_I of every lane that probed, in place: their slots are distinct
-            if ((probed >> l) & 1ull)
+            // UPDATE_I of every path lane before the cut; their slots are distinct
+            if ((path & keep) >> l & 1ull)
                 S.dict[slot] = (uint16_t)p;
             wave_order();
             if (done)
                 break;
-            ip += r > navail ? r : navail;
+            ip += end;
             if (ip >= ip_end)
                 break;
         }
