@@ -12,7 +12,8 @@ for rel in ("trace/bench_kernel_stats.csv", "pmc_fetch/fetch_counter_collection.
         shutil.copy(p, os.path.join(dst, os.path.basename(p)))
 stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(src, "trace/bench_kernel_stats.csv")))}
 dec = next(v for k, v in stats.items() if "decode_fast_kernel" in k)
-enc = next(v for k, v in stats.items() if "encode_kernel" in k)
+enc = next((v for k, v in stats.items() if "encode_fast_kernel" in k),
+           next(v for k, v in stats.items() if "encode_kernel" in k))
 def counter(path):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if "decode_fast" in r["Kernel_Name"]]
     return statistics.mean(vals), len(vals)
