@@ -1,32 +1,34 @@
 // lzo1x_decode_fast.hip -- the throughput LZO1X decoder for MI355X (gfx950).
 //
-// One 64-lane wave per block.  The compressed block is processed in pieces of
-// kPiece input bytes; each piece goes through:
+// One workgroup of two waves per block, working on pieces of kPiece bytes of
+// compressed input as a pipeline:
 //
-//  1. PARSE (lane = kSeg-byte input segment).  The LZO1X grammar
-//     (lib/minilzo.c:3308-3699) is a state machine
-//     over instruction starts (pos, state), state A (top), B (after a literal
-//     run) or C (after 1-3 trailing literals).  Every lane decodes
-//     speculatively from kLook bytes before its segment (state A, restarting
-//     one byte later whenever the guess runs into an impossible instruction)
-//     and marks the points it visits inside its segment.  Each lane then walks
-//     the TRUE path from its entry (its predecessor's exit) until it lands on
-//     one of its own marks (merged) or leaves the segment; the entry/exit
-//     chain is iterated until no entry changes (lane 0's entry is exact, so
-//     this converges; on real data speculation re-synchronises within a few
-//     instructions and one round suffices).  Two more walks count and write
-//     the ops (literal runs and matches) of the true path into an LDS op list
-//     in stream order.
+//  * PARSER wave (wave 1) finds the instructions of piece q+1.. while the
+//    executor runs piece q, and is also the block's only HBM writer.
+//    Parse (lane = kSeg-byte input segment): the LZO1X grammar
+//    (lib/minilzo.c:3308-3699) is a state machine
+//    over instruction starts (pos, state), state A (top), B (after a literal
+//    run) or C (after 1-3 trailing literals).  Every lane decodes
+//    speculatively from kLook bytes before its segment (state A, restarting
+//    one byte later whenever the guess runs into an impossible instruction)
+//    and marks the points it visits inside its segment.  Each lane then walks
+//    the TRUE path from its assumed entry (its predecessor's exit) until it
+//    lands on one of its own marks, and a scalar scan chains the true entries,
+//    walking exactly only where a guess was wrong.  Two more walks count and
+//    write the ops (literal runs and matches: length, source) of the true path
+//    to one of kSlots per-block op slots in global scratch.
+//    Writer duty, between parse steps: copy final output from the LDS ring to
+//    HBM in 1-KiB dwordx4 chunks; publish `issued` (ring slots reusable) at
+//    once and `landed` (readable from HBM) when the executor needs it.
 //
-//  2. EXECUTE (lane = op, then lane = 4-byte output unit).  64 ops at a time:
-//     a DPP prefix sum gives output offsets; the ops are cut into batches
-//     whose match sources all precede the batch (no dependency inside a
-//     batch), and each batch's output is produced 256 bytes per step: op
-//     starts are flagged per byte in LDS, a DPP scan of the per-unit flag
-//     counts gives every byte its op, and each lane gathers its 4 bytes
-//     (input staging / global input for literals; the LDS output ring or,
-//     beyond the ring, the already-stored HBM output for matches) and writes
-//     the dword to the ring and to HBM.
+//  * EXECUTOR wave (wave 0) issues no stores, so its loads never queue behind
+//    stores (gfx9 vmcnt retires a wave's loads and stores in one in-order
+//    queue).  Per 64 ops of a published piece: a DPP prefix sum gives output
+//    offsets; literal spans and far match sources are copied into an LDS
+//    source buffer with one batched load round trip; source forwarding and
+//    batches whose match sources all precede the batch; each batch is
+//    produced 256 bytes per step into the LDS output ring (op starts tagged
+//    per 4-byte chunk, a ballot maps every chunk to its op).
 //
 // Anything the fast path does not handle exactly (malformed input, lookbehind
 // or capacity errors, op-list overflow, EOF not at the end, misaligned
@@ -52,6 +54,11 @@ constexpr uint32_t kLook = POM_LOOK;             // speculative lead-in before a
 constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
 constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
+#ifndef POM_SLOTS
+#define POM_SLOTS 4
+#endif
+constexpr uint32_t kSlots = POM_SLOTS;           // parsed pieces the parser may run ahead
+static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_WRITER_SLEEP
 #define POM_WRITER_SLEEP 127                     // idle writer sleeps ~8K cycles between polls
 #endif
@@ -59,23 +66,28 @@ constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
 #define POM_FWD_ROUNDS 3                         // source-forwarding rounds per window
 #endif
 #ifndef POM_WAVES_PER_EU
-#define POM_WAVES_PER_EU 8                       // 16 blocks (decoder + writer wave) per CU
+#define POM_WAVES_PER_EU 8                       // 16 blocks (executor + parser wave) per CU
 #endif
 #ifndef POM_RING
 #define POM_RING 4096
 #endif
-constexpr uint32_t kRing = POM_RING;             // recent output kept in LDS
-constexpr uint32_t kRingSlack = kRing / 4;       // decoder keeps this much ring unflushed-free
-constexpr uint32_t kRingMask = kRing - 1;
-#ifndef POM_FAR
-#define POM_FAR 1024
+#ifndef POM_DUTY_EVERY
+#define POM_DUTY_EVERY 4                         // parser pass-1 iterations between writer duties
 #endif
-constexpr uint32_t kFarBytes = POM_FAR;          // per-window copy of far match sources
-constexpr uint32_t kFarDw = kFarBytes / 4;
-static_assert(kFarDw <= 4 * kWave, "far copy: at most 4 dwords per lane");
+constexpr uint32_t kRing = POM_RING;             // recent output kept in LDS
+constexpr uint32_t kRingMask = kRing - 1;
+#ifndef POM_SRCBUF
+#define POM_SRCBUF 1024
+#endif
+constexpr uint32_t kSrcBytes = POM_SRCBUF;       // per-window copy of literal spans and far sources
+constexpr uint32_t kSrcDw = kSrcBytes / 4;
+static_assert(kSrcDw <= 4 * kWave, "source copy: at most 4 dwords per lane");
 constexpr uint32_t kLitFlag = 0x80000000u;
+constexpr uint32_t kLinHbm = 0x4000;             // linear source addresses from here: input in HBM
 constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wrap 32 bits
 constexpr int32_t kFallback = 0x7FFF0001;        // status: exact decoder pending
+constexpr uint32_t kInfoEof = 1u << 16;          // piece info: the piece ends with EOF
+constexpr uint32_t kInfoErr = 1u << 17;          // piece info: the block needs the exact decoder
 
 // parse states (instruction starts)
 constexpr uint32_t ST_A = 0;   // top: t < 16 is a literal run
@@ -86,34 +98,36 @@ constexpr uint32_t kPosEnd = 0xFFFFFFF0u;        // exit marker: EOF reached / d
 constexpr uint32_t kPosUnknown = 0xFFFFFFE0u;    // speculative walk gave up
 
 struct __attribute__((aligned(16))) FastLds {
+    // executor
     uint32_t ring[kRing / 4];
-    uint32_t far[kFarDw];     // sources of this window's far matches (beyond the ring)
-    uint32_t stage[kStageBytes / 4];
-
-    uint4 wop[kWave];         // window op: {o, source base (| kLitFlag: LDS-linear), first chunk, L (| kLitFlag: needs HBM)}
+    uint32_t src[kSrcDw];     // this window's literal spans and far match sources
+    uint4 wop[kWave];         // window op: {o, source base (| kLitFlag: linear), first chunk, L (| kLitFlag: needs HBM)}
     uint2 wper[kWave];        // window op: {period, floor((2^32-1)/period)}
-    uint32_t flags[kWave];    // per-step chunk tags (far_issue: per-dword byte flags)
+    uint32_t flags[kWave];    // per-step chunk tags (src_issue: per-dword byte flags)
     uint32_t sink;            // target of masked-off byte writes
-    union {
-        uint8_t marks[kPiece];        // parse: speculative path marks (pass 1, merge)
-        uint16_t opref[kOpMax];       // then: the piece's ops as instruction references
-    };
-    // decoder -> writer hand-off (LDS words, workgroup scope)
-    uint32_t produced;      // output bytes final in the ring
-    uint32_t flushed;       // output bytes stored to HBM and landed
-    uint32_t state;         // 0 running, 1 finished, 2 refused
+    // parser
+    uint32_t stage[kStageBytes / 4];
+    uint8_t marks[kPiece];    // speculative path marks (pass 1, merge)
+    // hand-off words (LDS, workgroup scope)
+    uint32_t produced;        // executor -> writer: output bytes final in the ring
+    uint32_t issued;          // writer -> executor: stores issued (ring slots reusable)
+    uint32_t landed;          // writer -> executor: output bytes stored to HBM and landed
+    uint32_t need;            // executor -> writer: landed position it waits for
+    uint32_t state;           // executor -> parser: 0 running, 1 finished, 2 refused
+    uint32_t parsed;          // parser -> executor: pieces whose ops are in their slot
+    uint32_t consumed;        // executor -> parser: pieces whose slot is free again
+    uint32_t pinfo[kSlots];   // per slot: op count | kInfoEof | kInfoErr
 };
 
 constexpr uint32_t kRingOff = 0;                                  // offsetof(FastLds, ring)
-constexpr uint32_t kFarOff = kRing;                               // offsetof(FastLds, far)
-constexpr uint32_t kStageOff = kRing + kFarBytes;                 // offsetof(FastLds, stage)
+constexpr uint32_t kSrcOff = kRing;                               // offsetof(FastLds, src)
 static_assert(offsetof(FastLds, ring) == kRingOff, "layout");
-static_assert(offsetof(FastLds, far) == kFarOff, "layout");
-static_assert(offsetof(FastLds, stage) == kStageOff, "layout");
-constexpr uint32_t kSinkOff = kStageOff + kStageBytes + (kWave * (16 + 8 + 4));   // offsetof(FastLds, sink)
+static_assert(offsetof(FastLds, src) == kSrcOff, "layout");
+constexpr uint32_t kSinkOff = kSrcOff + kSrcBytes + (kWave * (16 + 8 + 4));   // offsetof(FastLds, sink)
 static_assert(offsetof(FastLds, sink) == kSinkOff, "layout");
 constexpr uint32_t kLdsMask = 0x3FFF;                              // LDS-linear address space
-static_assert(sizeof(FastLds) <= kLdsMask + 1, "linear LDS addresses are masked to 16 KiB");
+static_assert(sizeof(FastLds) <= kLdsMask + 1 && kLdsMask + 1 == kLinHbm,
+              "linear LDS addresses are masked to 16 KiB");
 // 16 blocks per CU share its 160 KiB of LDS
 static_assert(sizeof(FastLds) * 2 * POM_WAVES_PER_EU <= 160 * 1024, "LDS budget");
 
@@ -427,22 +441,6 @@ __device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
 }
 
 
-// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums (slots
-// 0..CN_FIRST-1) and event counts (CN_*) go to stamps[b * kStampSlots + i];
-// no output value depends on them.  scripts/diag_decode.py knows this order.
-enum { PH_STAGE, PH_PASS1, PH_PWALK, PH_MERGE, PH_COUNT, PH_WRITE,
-       PH_WLOAD, PH_WSCAN, PH_FARI, PH_FWD, PH_FARC, PH_BATCH,
-       PH_SPACE, PH_FLAGS, PH_GATHER, PH_PUB,
-       CN_FIRST, CN_WALKS = CN_FIRST, CN_WINDOWS, CN_FARWIN, CN_BATCHES, CN_STEPS,
-       CN_IT_PASS1, CN_IT_PWALK, CN_IT_WALK, CN_IT_COUNT, CN_IT_WRITE, CN_FWD_ROUNDS, PH_N };
-constexpr int kStampSlots = 32;
-static_assert(PH_N <= kStampSlots, "stamp slots per block");
-
-// Uniform walk of the true path from (pos, st) through lane i's segment
-// [c0, c1) until it lands on one of lane i's final-generation marks (then
-// lane i's speculative exit is the answer) or leaves the segment.
-// SPEC: per-lane speculative walk that gives up (pos = kPosUnknown) where the
-// exact slow decoder would be needed; the scalar scan then walks exactly.
 template <bool SPEC>
 __device__ __forceinline__ uint32_t walk_uniform(const FastLds& S, const Blk& k, uint32_t c0,
                                                  uint32_t c1, uint32_t gen, uint32_t xpos,
@@ -479,184 +477,23 @@ __device__ __forceinline__ uint32_t walk_uniform(const FastLds& S, const Blk& k,
     return steps;
 }
 
-// ---------------------------------------------------------------------------
-// Writer wave: copies final output from the LDS ring to HBM with 16-byte
-// stores, keeping a few chunks in flight; publishes `flushed` once stores have
-// landed.  It issues no loads, so its stores never hold up the decoder wave's
-// loads (gfx9 vmcnt retires loads and stores in one in-order queue per wave).
-// ---------------------------------------------------------------------------
-__device__ void writer_wave(FastLds& S, uint8_t* out, uint32_t l)
+// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums and event
+// counts go to stamps[b * kStampSlots + i]; no output value depends on them.
+// Each wave writes only the slots it owns (parser: kParserSlots).
+// scripts/diag_decode.py knows this order.
+enum { PH_STAGE, PH_PASS1, PH_PWALK, PH_MERGE, PH_COUNT, PH_WRITE, PH_PSLOT, PH_PDUTY,
+       PH_EWAIT, PH_WLOAD, PH_WSCAN, PH_FARI, PH_FWD, PH_FARC, PH_BATCH,
+       PH_SPACE, PH_FLAGS, PH_GATHER, PH_PUB,
+       CN_FIRST, CN_WALKS = CN_FIRST, CN_IT_PASS1, CN_IT_PWALK, CN_IT_WALK, CN_IT_COUNT,
+       CN_IT_WRITE, CN_PIECES,
+       CN_WINDOWS, CN_SRCWIN, CN_SRCMISS, CN_BATCHES, CN_STEPS, CN_FWD_ROUNDS, PH_N };
+constexpr int kStampSlots = 32;
+static_assert(PH_N <= kStampSlots, "stamp slots per block");
+__device__ __forceinline__ bool parser_slot(int i)
 {
-    constexpr uint32_t kChunk = 16 * kWave;        // 1 KiB per store instruction
-    uint32_t issued = 0;
-    uint32_t pend[2] = {0, 0};                     // ends of chunks in flight, oldest first
-    uint32_t npend = 0;
-    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
-        const uint32_t state = lds_load(&S.state);
-        const uint32_t prod = lds_load(&S.produced);
-        if (state == 2)
-            return;                                // refused: exact decoder redoes the block
-        const uint32_t upto = state == 1 ? prod : (prod & ~15u);
-        if (upto > issued && (upto - issued >= kChunk || state == 1)) {
-            const uint32_t end = upto - issued > kChunk ? issued + kChunk : upto;
-            const uint32_t x = issued + 16 * l;
-            if (x + 16 <= end) {
-                const uint32_t i = x & kRingMask;
-                const uint4 v = *(const uint4*)&S.ring[i >> 2];
-                *(uint4*)(out + x) = v;
-            } else if (x < end) {
-                for (uint32_t q = 0; x + q < end; q++)
-                    out[x + q] = (uint8_t)ring_byte(S, x + q);
-            }
-            issued = end;
-            if (npend == 2) {
-                __builtin_amdgcn_s_waitcnt(0x0F71);        // vmcnt(1): oldest chunk landed
-                lds_store(&S.flushed, pend[0]);
-                pend[0] = pend[1];
-                npend = 1;
-            }
-            pend[npend++] = end;
-            continue;
-        }
-        if (npend) {                               // nothing new: drain and publish
-            __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
-            lds_store(&S.flushed, issued);
-            npend = 0;
-            continue;
-        }
-        if (state == 1)
-            return;
-        // Poll rarely: the scalar unit is shared by every wave of the CU, and a
-        // tight poll loop costs the decoder waves their SALU issue slots.  (The
-        // ring's 3 KiB of headroom covers ~8K cycles of decoder output; waking
-        // the writer with s_wakeup per ready chunk measured slower than
-        // letting it drain several chunks per poll.)
-        __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
-    }
+    return i <= PH_PDUTY || (i >= CN_WALKS && i <= CN_PIECES);
 }
 
-// ---------------------------------------------------------------------------
-// Far sources.  A match whose source may have left the ring by the time its
-// step runs would read HBM byte by byte in every step it touches (61% of the
-// steps of an ITB block).  Instead its whole source span is copied once per
-// window into S.far -- one batched global round trip -- and the op becomes an
-// LDS-linear source like a literal.  Called after forwarding, with the window
-// ops' output offset o, length L, period dp and source b (in/out).
-//
-// Where the bytes are at this point (carry = output before this window): the
-// last step of the previous window ended at most 255 bytes past carry, so the
-// ring still holds every position >= carry + 255 - kRing, and its space check
-// left flushed >= carry - kRing + kRingSlack, so every position below that is
-// in HBM.  Sources lie below carry (db + span <= carry is required).
-// ---------------------------------------------------------------------------
-// Far ops are never forwarded (their sources lie below the window), so the
-// copy is issued before forwarding -- which then hands far-buffer sources on
-// to the ops that forward to them -- and only committed to LDS after it, so
-// the loads' latency hides under the forwarding rounds.
-struct FarCopy {
-    uint32_t v[4];          // this lane's buffer dwords 4l .. 4l+3
-    uint32_t used;          // buffer dwords filled (0: no far op in the window)
-};
-
-__device__ __forceinline__ FarCopy far_issue(FastLds& S, const Blk& k, uint32_t l,
-                                             uint32_t nwin, uint32_t carry, uint32_t o,
-                                             uint32_t L, uint32_t dp, uint32_t& db)
-{
-    FarCopy fc;
-    fc.used = 0;
-    const uint32_t span = dp ? dp : L;
-    // some byte may read below the ring: sp + kRing < step_end + 4 with
-    // step_end <= x + 259 and sp - db <= x - o (p == 0) or < p
-    const bool far = l < nwin && !(db & kLitFlag) && db + span <= carry &&
-                     db + kRing < o + (dp ? L : 0u) + 260u;
-    if (!wave_ballot(far))
-        return fc;
-    const uint32_t nd = far ? ((db + span + 3u) >> 2) - (db >> 2) : 0u;
-    const uint32_t cum = wave_incl_scan(nd);
-    const bool acc = far && cum <= kFarDw;                  // the buffer takes a prefix of them
-    const uint32_t acc_nd = acc ? nd : 0u;
-    const uint64_t accm = wave_ballot(acc);
-    const uint32_t used = accm ? lane_read(cum, 63u - (uint32_t)__builtin_clzll(accm)) : 0u;
-    fc.used = used;
-    if (!used)
-        return fc;
-    const uint32_t gl_end = carry + kRingSlack - kRing;     // below: in HBM (may wrap: none)
-    const bool gl_any = carry + kRingSlack > kRing;
-    // Buffer dword t -> its op, as in the gather steps: flag each op's first
-    // buffer dword (S.flags, one byte per dword), scan the flag counts; the
-    // k-th op's (source dword - buffer dword) sits in a table at k (the
-    // window's op records are not written yet, so their space is free).
-    uint32_t* const delta = (uint32_t*)S.wop;
-    S.flags[l] = 0;
-    wave_order();
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(accm >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)accm, 0u));
-    if (acc_nd) {
-        ((uint8_t*)S.flags)[cum - acc_nd] = 1;
-        delta[rank] = (db >> 2) - (cum - acc_nd);
-    }
-    wave_order();
-    const uint32_t f = S.flags[l];
-    const uint32_t nst = (uint32_t)__builtin_popcount(f);
-    const uint32_t jb = wave_incl_scan(nst) - nst - 1u;      // ops starting before 4l, minus 1
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) {
-        const uint32_t t = l * 4 + i;                        // buffer dword
-        const uint32_t j = (jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * i)) - 1u))) & 63u;
-        const uint32_t a = (t + delta[j]) * 4u;              // output byte offset, aligned
-        const bool need = t < used;
-        const bool hbm = need && gl_any && a + 4u <= gl_end;
-        fc.v[i] = S.ring[(a & kRingMask) >> 2];
-        if (hbm)
-            fc.v[i] = __builtin_nontemporal_load((gdword*)(k.out + a));
-    }
-    if (acc_nd)
-        db = kLitFlag | (kFarOff + 4u * (cum - acc_nd) + (db & 3u));
-    return fc;
-}
-
-__device__ __forceinline__ void far_commit(FastLds& S, uint32_t l, const FarCopy& fc)
-{
-    if (!fc.used)
-        return;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++)
-        if (l * 4 + i < fc.used)
-            S.far[l * 4 + i] = fc.v[i];
-}
-
-// ---------------------------------------------------------------------------
-template <bool STAMPS>
-__global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
-    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-    uint32_t* __restrict__ fallback, uint32_t nblocks, uint64_t* __restrict__ stamps)
-{
-    __shared__ FastLds S;
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks)
-        return;
-    const uint32_t l = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x == 0) {
-        S.produced = 0;
-        S.flushed = 0;
-        S.state = 0;
-    }
-    if (threadIdx.x < kWave)
-        S.flags[threadIdx.x] = 0;             // chunk tags start at 0x80000001
-    __syncthreads();
-    uint8_t* const out = dst + dst_off[b];
-    if (wave == 1) {
-        // The decoder refuses misaligned destinations before publishing anything.
-        writer_wave(S, out, l);
-        return;
-    }
-
-    uint64_t acc[PH_N] = {};
-    uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #define STAMP(ph)                                                   \
     do {                                                            \
         if (STAMPS) {                                               \
@@ -666,247 +503,581 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         }                                                           \
     } while (0)
 
-    Blk k;
-    k.in = src + src_off[b];
-    k.z = src_len[b];
-    k.out = out;
-    k.cap = dst_cap[b];
-    k.P = 0;
-    k.staged = 0;
+// ---------------------------------------------------------------------------
+// Writer duty (parser wave, between parse steps): final ring bytes go to HBM
+// in 1-KiB chunks, one dwordx4 store per lane.  Two positions are published:
+//   issued  -- stores issued (their data left the ring): those ring slots
+//              may be overwritten;
+//   landed  -- stores known to be in HBM: that output may be read back.
+// `landed` trails by one batch of chunks: the wait for a batch is taken when
+// the next one is issued (by then it has long landed), or at once when the
+// executor asks for more (S.need) -- so the executor never waits on a store
+// it does not read.
+// Returns 2 once the executor refused the block, 1 once everything it
+// produced has landed after it finished, 0 otherwise.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kChunk = 16 * kWave;          // 1 KiB per store instruction
 
-    // The exact decoder takes: destinations not 16-byte aligned, empty or huge
-    // blocks (lengths up to 255 * z must not wrap 32 bits).
-    bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
+struct WState {
+    uint32_t issued;        // output bytes whose stores were issued
+    uint32_t landed;        // output bytes published as landed
+};
+
+__device__ __forceinline__ uint32_t writer_duty(FastLds& S, uint8_t* out, uint32_t l, WState& w)
+{
+    const uint32_t state = lds_load(&S.state);
+    const uint32_t prod = lds_load(&S.produced);
+    if (state == 2)
+        return 2;                                      // refused: the exact decoder redoes it
+    const uint32_t upto = state == 1 ? prod : (prod & ~(kChunk - 1));
+    const bool fresh = upto > w.issued;
+    if (w.landed < w.issued && (fresh || state == 1 || lds_load(&S.need) > w.landed)) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): the last batch landed
+        w.landed = w.issued;
+        lds_store(&S.landed, w.landed);
+    }
+    if (!fresh)
+        return (state == 1 && w.landed == prod) ? 1u : 0u;
+    for (int c = 0; c < 4 && w.issued < upto; c++) {
+        const uint32_t end = upto - w.issued > kChunk ? w.issued + kChunk : upto;
+        const uint32_t x = w.issued + 16 * l;
+        if (x + 16 <= end) {
+            const uint32_t i = x & kRingMask;
+            const uint4 v = *(const uint4*)&S.ring[i >> 2];
+            *(uint4*)(out + x) = v;
+        } else if (x < end) {
+            for (uint32_t q = 0; x + q < end; q++)
+                out[x + q] = (uint8_t)ring_byte(S, x + q);
+        }
+        w.issued = end;
+    }
+    lds_store(&S.issued, w.issued);                    // (after the ring reads completed)
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Parser wave: pieces in stream order with exact entries (the true exit of
+// the previous piece), ops to slot q mod kSlots; writer duty in between.
+// ---------------------------------------------------------------------------
+template <bool STAMPS>
+__device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict__ gops, uint32_t l,
+                            uint64_t* acc)
+{
+    uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    WState w;
+    w.issued = 0;
+    w.landed = 0;
     uint32_t entry_pos = 0, entry_st = ST_F;   // true entry of the current piece
-    uint32_t carry = 0;                        // output produced so far
-    uint32_t flushed_seen = 0;                 // last `flushed` read
-    uint32_t tag = 0;                          // step counter for the chunk tags
-    bool done = false;                         // EOF consumed
-
-    while (!refuse && !done) {
+    for (uint32_t q = 0;; q++) {
         // Skip pieces in which no instruction starts (inside a long literal run).
         if (entry_pos >= k.P + kPiece)
             k.P = entry_pos - (entry_pos % kPiece);
-        if (k.P >= k.z) {                      // ran off the end without EOF
-            refuse = true;
-            break;
+        // a free slot: the executor is done with piece q - kSlots
+        for (uint32_t spin = 0; q - lds_load(&S.consumed) >= kSlots; spin++) {
+            if (writer_duty(S, k.out, l, w) == 2 || spin > (1u << 22))
+                return;                        // the executor refused (or is stuck)
+            __builtin_amdgcn_s_sleep(2);
         }
-        // ---- stage the piece's input --------------------------------------
-        {
+        STAMP(PH_PSLOT);
+        if (STAMPS)
+            acc[CN_PIECES] += 1;
+        uint2* const slot = gops + (q & (kSlots - 1)) * kOpMax;
+        bool err = k.P >= k.z;                 // ran off the end without EOF
+        bool eof = false;
+        uint32_t total_ops = 0;
+        uint32_t next_pos = 0, next_st = 0;
+        if (!err) {
+            // ---- stage the piece's input --------------------------------------
             const uint32_t avail = k.z - k.P;
             k.staged = avail < kStageBytes ? avail : kStageBytes;
             const uint8_t* base = k.in + k.P;
             for (uint32_t i = l * 4; i < kStageBytes; i += kWave * 4) {
-                uint32_t w = 0;
+                uint32_t v = 0;
                 if (i + 4 <= k.staged)
-                    w = global_dword<false>(base + i);
+                    v = global_dword<false>(base + i);
                 else
                     for (uint32_t j = i; j < k.staged; j++)
-                        w |= (uint32_t)base[j] << (8 * (j - i));
-                S.stage[i >> 2] = w;
+                        v |= (uint32_t)base[j] << (8 * (j - i));
+                S.stage[i >> 2] = v;
             }
             for (uint32_t i = l * 4; i < kPiece; i += kWave * 4)
                 *(uint32_t*)&S.marks[i] = 0;
-        }
-        wave_order();
-        STAMP(PH_STAGE);
-        const uint32_t c0 = k.P + l * kSeg;            // this lane's segment
-        const uint32_t c1 = c0 + kSeg;
+            wave_order();
+            STAMP(PH_STAGE);
+            const uint32_t c0 = k.P + l * kSeg;        // this lane's segment
+            const uint32_t c1 = c0 + kSeg;
 
-        // ---- pass 1: speculative walk, mark visited points -------------------
-        // A mark is (state + 1) | (gen << 2); gen counts this lane's restarts,
-        // and only marks of the final generation lie on the path that really
-        // reaches xpos (a restart breaks the chain).
-        uint32_t xpos, xst, xgen = 0;
-        uint32_t it_local = 0;                         // (diagnostics)
-        if (c1 <= entry_pos) {                         // no instruction starts here
-            xpos = entry_pos;
-            xst = entry_st;
-        } else {
+            // ---- pass 1: speculative walk, mark visited points ---------------
+            // A mark is (state + 1) | (gen << 2); gen counts this lane's
+            // restarts, and only marks of the final generation lie on the path
+            // that really reaches xpos (a restart breaks the chain).
+            const bool p1 = c1 > entry_pos;            // else no instruction starts here
             uint32_t pos = c0 >= k.P + kLook ? c0 - kLook : k.P;
             if (pos < entry_pos)
                 pos = entry_pos;
             uint32_t st = pos == entry_pos ? entry_st : ST_A;
             uint32_t gen = 0;
-            while (pos < c1 && pos < k.z) {
-                if (STAMPS)
-                    it_local++;
-                if (pos >= c0)
-                    S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 2));
-                bool slow = false;
-                const Step r = decode_step<true>(S, k, pos, st, &slow);
-                if (r.bad || r.eof) {                  // impossible guess: restart later
-                    pos++;
-                    st = ST_A;
-                    gen = gen < 63 ? gen + 1 : 63;
-                    continue;
-                }
-                pos = r.pos;
-                st = r.st;
-            }
-            xpos = pos >= k.z ? kPosEnd : pos;
-            xst = st;
-            xgen = gen < 63 ? gen : 0xFFu;             // saturated: never merge
-        }
-        wave_order();
-        STAMP(PH_PASS1);
-
-        // ---- true entries: one parallel walk from the assumed entries, then a
-        // scalar scan that reuses it and walks only where the guess was wrong.
-        const uint32_t apos = shift_up1(xpos, entry_pos), ast = shift_up1(xst, entry_st);
-        uint32_t fpos = apos, fst = ast;
-        if (STAMPS)
-            acc[CN_IT_PASS1] += wave_max_dbg(it_local);
-        {
-            const uint32_t ws = walk_uniform<true>(S, k, c0, c1, xgen, xpos, xst, fpos, fst);   // per lane (divergent)
-            if (STAMPS)
-                acc[CN_IT_PWALK] += wave_max_dbg(ws);
-        }
-        STAMP(PH_PWALK);
-        // The scan visits only the lanes that need it.  Where lane i's true
-        // entry E equals its assumed one, lanes i, i+1, ... stay right as long
-        // as each walk landed on the next lane's assumed entry (f_l == x_l)
-        // and none gave up, so the scan jumps to the first lane q where that
-        // fails: mm (lane q-1's walk missed lane q's assumed entry) or uk
-        // (lane q's own walk gave up), with E_q = f_{q-1}.
-        uint32_t epos = apos, est = ast;
-        {
-            const uint64_t mm = wave_ballot(fpos != xpos || fst != xst) << 1;
-            const uint64_t uk = wave_ballot(fpos == kPosUnknown);
-            uint32_t E = entry_pos, Est = entry_st;
-            uint32_t i = 0;
-            while (i < (uint32_t)kWave) {
-                if (E == lane_read(apos, i) && Est == lane_read(ast, i)) {
-                    const uint64_t from_i = ~0ull << i;
-                    const uint64_t cand = (mm & (from_i << 1)) | (uk & from_i);
-                    if (!cand) {                       // right through lane 63
-                        E = lane_read(fpos, kWave - 1);
-                        Est = lane_read(fst, kWave - 1);
-                        break;
-                    }
-                    const uint32_t q = (uint32_t)__builtin_ctzll(cand);
-                    if (q > i) {
-                        E = lane_read(fpos, q - 1);
-                        Est = lane_read(fst, q - 1);
-                        i = q;
-                    }
-                }
-                // lane i on its own, from its true entry E
-                if (l == i) {
-                    epos = E;
-                    est = Est;
-                }
-                const uint32_t ci1 = k.P + (i + 1) * kSeg;
-                if (E < ci1) {                         // else: segment i has no true start
-                    if (E == lane_read(apos, i) && Est == lane_read(ast, i) &&
-                        lane_read(fpos, i) != kPosUnknown) {
-                        E = lane_read(fpos, i);
-                        Est = lane_read(fst, i);
+            for (uint32_t it = 1;; it++) {
+                const bool act = p1 && pos < c1 && pos < k.z;
+                if (!wave_ballot(act))
+                    break;
+                if (act) {
+                    if (pos >= c0)
+                        S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 2));
+                    bool slow = false;
+                    const Step r = decode_step<true>(S, k, pos, st, &slow);
+                    if (r.bad || r.eof) {              // impossible guess: restart later
+                        pos++;
+                        st = ST_A;
+                        gen = gen < 63 ? gen + 1 : 63;
                     } else {
-                        const uint32_t ws = walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i),
-                                                                lane_read(xpos, i), lane_read(xst, i), E, Est);
-                        if (STAMPS) {
-                            acc[CN_WALKS] += 1;
-                            acc[CN_IT_WALK] += ws;
+                        pos = r.pos;
+                        st = r.st;
+                    }
+                }
+                if (STAMPS)
+                    acc[CN_IT_PASS1] += 1;
+                if (it % POM_DUTY_EVERY == 0) {
+                    STAMP(PH_PASS1);
+                    if (writer_duty(S, k.out, l, w) == 2)
+                        return;
+                    STAMP(PH_PDUTY);
+                }
+            }
+            const uint32_t xpos = !p1 ? entry_pos : pos >= k.z ? kPosEnd : pos;
+            const uint32_t xst = !p1 ? entry_st : st;
+            const uint32_t xgen = !p1 ? 0u : gen < 63 ? gen : 0xFFu;   // saturated: never merge
+            wave_order();
+            STAMP(PH_PASS1);
+
+            // ---- true entries: one parallel walk from the assumed entries, then
+            // a scalar scan that reuses it and walks only where the guess was wrong.
+            const uint32_t apos = shift_up1(xpos, entry_pos), ast = shift_up1(xst, entry_st);
+            uint32_t fpos = apos, fst = ast;
+            {
+                const uint32_t ws = walk_uniform<true>(S, k, c0, c1, xgen, xpos, xst, fpos, fst);
+                if (STAMPS)
+                    acc[CN_IT_PWALK] += wave_max_dbg(ws);
+            }
+            STAMP(PH_PWALK);
+            if (writer_duty(S, k.out, l, w) == 2)
+                return;
+            STAMP(PH_PDUTY);
+            // Where lane i's true entry E equals its assumed one, lanes i, i+1,
+            // ... stay right as long as each walk landed on the next lane's
+            // assumed entry (f_l == x_l) and none gave up, so the scan jumps to
+            // the first lane q where that fails: mm (lane q-1's walk missed lane
+            // q's assumed entry) or uk (lane q's own walk gave up), E_q = f_{q-1}.
+            uint32_t epos = apos, est = ast;
+            {
+                const uint64_t mm = wave_ballot(fpos != xpos || fst != xst) << 1;
+                const uint64_t uk = wave_ballot(fpos == kPosUnknown);
+                uint32_t E = entry_pos, Est = entry_st;
+                uint32_t i = 0;
+                while (i < (uint32_t)kWave) {
+                    if (E == lane_read(apos, i) && Est == lane_read(ast, i)) {
+                        const uint64_t from_i = ~0ull << i;
+                        const uint64_t cand = (mm & (from_i << 1)) | (uk & from_i);
+                        if (!cand) {                   // right through lane 63
+                            E = lane_read(fpos, kWave - 1);
+                            Est = lane_read(fst, kWave - 1);
+                            break;
+                        }
+                        const uint32_t qq = (uint32_t)__builtin_ctzll(cand);
+                        if (qq > i) {
+                            E = lane_read(fpos, qq - 1);
+                            Est = lane_read(fst, qq - 1);
+                            i = qq;
                         }
                     }
+                    // lane i on its own, from its true entry E
+                    if (l == i) {
+                        epos = E;
+                        est = Est;
+                    }
+                    const uint32_t ci1 = k.P + (i + 1) * kSeg;
+                    if (E < ci1) {                     // else: segment i has no true start
+                        if (E == lane_read(apos, i) && Est == lane_read(ast, i) &&
+                            lane_read(fpos, i) != kPosUnknown) {
+                            E = lane_read(fpos, i);
+                            Est = lane_read(fst, i);
+                        } else {
+                            const uint32_t ws = walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i),
+                                                                    lane_read(xpos, i), lane_read(xst, i), E, Est);
+                            if (STAMPS) {
+                                acc[CN_WALKS] += 1;
+                                acc[CN_IT_WALK] += ws;
+                            }
+                            STAMP(PH_MERGE);
+                            if (writer_duty(S, k.out, l, w) == 2)
+                                return;
+                            STAMP(PH_PDUTY);
+                        }
+                    }
+                    i++;
                 }
-                i++;
+                next_pos = E;                          // (uniform: the piece's true exit)
+                next_st = Est;
             }
-            fpos = E;                                  // (uniform: the piece's true exit)
-            fst = Est;
-        }
-        const uint32_t next_pos = fpos, next_st = fst;
-        STAMP(PH_MERGE);
+            STAMP(PH_MERGE);
 
-        // ---- pass 3: count ops of the true path ------------------------------
-        uint32_t nops = 0;
-        bool lane_eof = false, lane_err = false;
-        {
-            uint32_t pos = epos, st = est;
-            uint32_t itc = 0;
-            while (pos < c1) {
-                itc++;
-                const Step r = decode_step(S, k, pos, st);
-                if (r.bad) {
-                    lane_err = true;
-                    break;
+            // ---- pass 3: count ops of the true path ------------------------------
+            uint32_t nops = 0;
+            bool lane_eof = false, lane_err = false;
+            {
+                uint32_t p = epos, s = est;
+                uint32_t itc = 0;
+                while (p < c1) {
+                    itc++;
+                    const Step r = decode_step(S, k, p, s);
+                    if (r.bad) {
+                        lane_err = true;
+                        break;
+                    }
+                    if (r.eof) {                       // EOF carries no op
+                        lane_eof = true;
+                        break;
+                    }
+                    if (r.aL > kMaxOpLen || r.bL > kMaxOpLen) {
+                        lane_err = true;
+                        break;
+                    }
+                    nops += (r.aL ? 1u : 0u) + (r.bL ? 1u : 0u);
+                    p = r.pos;
+                    s = r.st;
                 }
-                if (r.eof) {                           // EOF carries no op
-                    lane_eof = true;
-                    break;
-                }
-                if (r.aL > kMaxOpLen || r.bL > kMaxOpLen) {
-                    lane_err = true;
-                    break;
-                }
-                nops += (r.aL ? 1u : 0u) + (r.bL ? 1u : 0u);
-                pos = r.pos;
-                st = r.st;
+                if (STAMPS)
+                    acc[CN_IT_COUNT] += wave_max_dbg(itc);
             }
-            if (STAMPS)
-                acc[CN_IT_COUNT] += wave_max_dbg(itc);
-        }
-        if (wave_ballot(lane_err)) {
-            refuse = true;
-            break;
-        }
-        const uint32_t incl = wave_incl_scan(nops);
-        const uint32_t total_ops = lane_read(incl, kWave - 1);
-        STAMP(PH_COUNT);
-        if (total_ops > kOpMax) {
-            refuse = true;
-            break;
-        }
-        // ---- pass 4: write the ops --------------------------------------------
-        {
-            uint32_t w = incl - nops;
-            uint32_t pos = epos, st = est;
-            uint32_t itw = 0;
-            while (pos < c1) {
-                itw++;
-                const Step r = decode_step(S, k, pos, st);
-                if (r.eof)
-                    break;
-                // An op is stored as a reference to its instruction
-                // (piece offset | state << 10 | part << 12, part 1 = trailing
-                // literals; instructions start inside the 1-KiB piece) and is
-                // re-decoded when its window executes: 2 bytes of LDS, not 8.
-                const uint32_t ref = (pos - k.P) | (st << 10);
-                if (r.aL)
-                    S.opref[w++] = (uint16_t)ref;
-                if (r.bL)
-                    S.opref[w++] = (uint16_t)(ref | (1u << 12));
-                pos = r.pos;
-                st = r.st;
+            const uint32_t incl = wave_incl_scan(nops);
+            total_ops = lane_read(incl, kWave - 1);
+            err = wave_ballot(lane_err) != 0 || total_ops > kOpMax;
+            eof = wave_ballot(lane_eof) != 0;
+            STAMP(PH_COUNT);
+            if (writer_duty(S, k.out, l, w) == 2)
+                return;
+            STAMP(PH_PDUTY);
+            // ---- pass 4: write the ops (length, source) to the slot ---------------
+            if (!err) {
+                uint32_t wi = incl - nops;
+                uint32_t p = epos, s = est;
+                uint32_t itw = 0;
+                while (p < c1) {
+                    itw++;
+                    const Step r = decode_step(S, k, p, s);
+                    if (r.eof)
+                        break;
+                    if (r.aL)
+                        slot[wi++] = make_uint2(r.aL, r.aS);
+                    if (r.bL)
+                        slot[wi++] = make_uint2(r.bL, r.bS);
+                    p = r.pos;
+                    s = r.st;
+                }
+                if (STAMPS)
+                    acc[CN_IT_WRITE] += wave_max_dbg(itw);
             }
-            if (STAMPS)
-                acc[CN_IT_WRITE] += wave_max_dbg(itw);
+            if (!eof && next_pos == kPosEnd)
+                err = true;                            // dead without EOF
+            STAMP(PH_WRITE);
         }
-        wave_order();
+        // publish piece q once its op records landed
+        __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
+        lds_store(&S.pinfo[q & (kSlots - 1)],
+                  total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u));
+        lds_store(&S.parsed, q + 1);
         STAMP(PH_WRITE);
-        if (wave_ballot(lane_eof))
-            done = true;
-        else {
-            entry_pos = next_pos;                      // next piece: the true exit
-            entry_st = next_st;
-            if (entry_pos == kPosEnd) {                // dead without EOF
+        if (err || eof)
+            break;
+        entry_pos = next_pos;                          // next piece: the true exit
+        entry_st = next_st;
+        k.P += kPiece;
+        if (writer_duty(S, k.out, l, w) == 2)
+            return;
+        STAMP(PH_PDUTY);
+    }
+    // parse finished: writer only
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+        if (writer_duty(S, k.out, l, w) != 0)
+            break;
+        __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
+    }
+    STAMP(PH_PSLOT);
+}
+
+// ---------------------------------------------------------------------------
+// Source buffer (executor).  Literal runs and far matches (whose source may
+// have left the ring by the time their step runs) get their source span
+// copied into S.src once per window -- one batched global round trip -- and
+// then read LDS like everything else.  Literal spans come first (they are
+// short), then far sources, each class a prefix in window order while the
+// buffer lasts.  Ops that do not fit read HBM byte by byte in their steps:
+// literals through linear addresses from kLinHbm (input position + kLinHbm).
+//
+// Where output bytes are (carry = output before this window): the ring holds
+// every position >= carry - kRing, and the executor waited for `landed` >=
+// carry - kRing, so every position below `landed` is in HBM.  Sources lie
+// below carry (db + span <= carry is required).
+// Far ops are never forwarded (their sources lie below the window), so the
+// copy is issued before forwarding -- which then hands buffer sources on to
+// the ops that forward to them -- and only committed to LDS after it, so the
+// loads' latency hides under the forwarding rounds.
+// ---------------------------------------------------------------------------
+// Executor: waits until the writer published landed >= need (asking for it
+// through S.need).
+__device__ __forceinline__ uint32_t wait_landed(FastLds& S, uint32_t need, uint32_t seen,
+                                                bool& refuse)
+{
+    if (seen >= need)
+        return seen;
+    seen = lds_load(&S.landed);
+    if (seen >= need)
+        return seen;
+    lds_store(&S.need, need);
+    for (uint32_t spin = 0; seen < need; spin++) {
+        if (spin > (1u << 22)) {               // writer stuck: let the exact path redo it
+            refuse = true;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        seen = lds_load(&S.landed);
+    }
+    return seen;
+}
+
+struct SrcCopy {
+    uint32_t v[4];          // this lane's buffer dwords 4l .. 4l+3 (first aligned dword)
+    uint32_t v1[4];         // (the next aligned dword, for unaligned input)
+    uint32_t sh;            // funnel shift of dword i at bits 2i..2i+1
+    uint32_t used;          // buffer dwords filled (0: nothing copied)
+    bool miss;              // (diagnostics) some candidate did not fit
+};
+
+__device__ __forceinline__ SrcCopy src_issue(FastLds& S, const Blk& k, uint32_t l, uint32_t nwin,
+                                             uint32_t carry, uint32_t landed, uint32_t o,
+                                             uint32_t L, uint32_t dp,
+                                             bool lit, uint32_t ipos, uint32_t& db)
+{
+    SrcCopy fc;
+    fc.used = 0;
+    fc.miss = false;
+    const uint32_t span = dp ? dp : L;
+    const bool litc = l < nwin && lit && L != 0;
+    // some byte may read below the ring: sp + kRing < step_end + 4 with
+    // step_end <= x + 259 and sp - db <= x - o (p == 0) or < p
+    const bool far = l < nwin && !lit && db + span <= carry &&
+                     db + kRing < o + (dp ? L : 0u) + 260u;
+    if (!wave_ballot(litc || far))
+        return fc;
+    const uint32_t sdw = litc ? ipos >> 2 : db >> 2;           // first source dword
+    const uint32_t nd_lit = litc ? ((ipos + L + 3u) >> 2) - sdw : 0u;
+    const uint32_t nd_far = far ? ((db + span + 3u) >> 2) - sdw : 0u;
+    const uint32_t cl = wave_incl_scan(nd_lit);
+    const uint32_t lit_total = lane_read(cl, kWave - 1);
+    const uint32_t cf = wave_incl_scan(nd_far) + lit_total;
+    const uint32_t nd = nd_lit + nd_far;
+    const uint32_t cum = litc ? cl : cf;
+    const bool acc = (litc || far) && cum <= kSrcDw;          // the buffer takes a prefix of each
+    const uint64_t accl = wave_ballot(acc && litc);
+    const uint64_t accf = wave_ballot(acc && far);
+    fc.miss = wave_ballot((litc || far) && !acc) != 0;
+    if (!(accl | accf))
+        return fc;
+    const uint32_t used_l = accl ? lane_read(cl, 63u - (uint32_t)__builtin_clzll(accl)) : 0u;
+    const uint32_t used_f = accf ? lane_read(cf, 63u - (uint32_t)__builtin_clzll(accf)) : lit_total;
+    const uint32_t used = accf ? used_f : used_l;
+    fc.used = used;
+    // Buffer dword t -> its op, as in the gather steps: flag each op's first
+    // buffer dword (S.flags, one byte per dword), scan the flag counts; the
+    // r-th op in buffer order has (source dword - buffer dword) at delta[r],
+    // bit 31 set for an input source (the window's op records are not written
+    // yet, so their space is free).
+    uint32_t* const delta = (uint32_t*)S.wop;
+    S.flags[l] = 0;
+    wave_order();
+    const uint32_t nl = (uint32_t)__builtin_popcountll(accl);
+    const uint32_t rank = litc
+        ? __builtin_amdgcn_mbcnt_hi((uint32_t)(accl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)accl, 0u))
+        : nl + __builtin_amdgcn_mbcnt_hi((uint32_t)(accf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)accf, 0u));
+    if (acc) {
+        ((uint8_t*)S.flags)[cum - nd] = 1;
+        delta[rank] = ((sdw - (cum - nd)) & 0x7FFFFFFFu) | (litc ? 0x80000000u : 0u);
+    }
+    wave_order();
+    const uint32_t f = S.flags[l];
+    const uint32_t nst = (uint32_t)__builtin_popcount(f);
+    const uint32_t jb = wave_incl_scan(nst) - nst - 1u;      // ops starting before 4l, minus 1
+    // every load first, then the funnels: one batched round trip
+    const uintptr_t in_last = ((uintptr_t)k.in + k.z - 1) & ~(uintptr_t)3;   // last dword with input
+    uint32_t w0[4], w1[4], sh[4];
+    bool hbm[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        const uint32_t t = l * 4 + i;                        // buffer dword
+        const uint32_t j = (jb + (uint32_t)__builtin_popcount(f & ((2u << (8 * i)) - 1u))) & 63u;
+        const uint32_t dj = delta[j];
+        const uint32_t a = ((t + dj) & 0x3FFFFFFFu) * 4u;   // source byte offset, dword aligned
+        const bool need = t < used;
+        const bool in_src = (dj & 0x80000000u) != 0;
+        // input: any byte address (two aligned dwords, the second only while it
+        // holds input); output: 16-byte aligned, below `landed` in HBM
+        const uintptr_t pa = (uintptr_t)(in_src ? k.in + a : k.out + a);
+        const uintptr_t qa = pa & ~(uintptr_t)3;
+        sh[i] = (uint32_t)(pa & 3);
+        hbm[i] = need && (in_src || a + 4u <= landed);
+        const uintptr_t qb = in_src && qa + 4 <= in_last ? qa + 4 : qa;
+        w0[i] = S.ring[(a & kRingMask) >> 2];
+        w1[i] = 0;
+        if (hbm[i]) {
+            w0[i] = __builtin_nontemporal_load((gdword*)qa);
+            w1[i] = __builtin_nontemporal_load((gdword*)qb);
+        }
+    }
+    // (funnels in src_commit: the loads' latency hides under forwarding)
+    fc.sh = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        fc.v[i] = w0[i];
+        fc.v1[i] = w1[i];
+        fc.sh |= (hbm[i] ? sh[i] : 0u) << (2 * i);
+    }
+    if (acc)
+        db = kLitFlag | (kSrcOff + 4u * (cum - nd) + ((litc ? ipos : db) & 3u));
+    return fc;
+}
+
+__device__ __forceinline__ void src_commit(FastLds& S, uint32_t l, const SrcCopy& fc)
+{
+    if (!fc.used)
+        return;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        const uint32_t sh = (fc.sh >> (2 * i)) & 3u;
+        if (l * 4 + i < fc.used)
+            S.src[l * 4 + i] = sh ? funnel(fc.v[i], fc.v1[i], sh) : fc.v[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+template <bool STAMPS>
+__global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+    uint32_t* __restrict__ fallback, uint2* __restrict__ ops, uint32_t nblocks,
+    uint64_t* __restrict__ stamps)
+{
+    __shared__ FastLds S;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t l = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x == 0) {
+        S.produced = 0;
+        S.issued = 0;
+        S.landed = 0;
+        S.need = 0;
+        S.state = 0;
+        S.parsed = 0;
+        S.consumed = 0;
+    }
+    if (threadIdx.x < kWave)
+        S.flags[threadIdx.x] = 0;             // chunk tags start at 0x80000001
+    __syncthreads();
+
+    uint64_t acc[PH_N] = {};
+    Blk k;
+    k.in = src + src_off[b];
+    k.z = src_len[b];
+    k.out = dst + dst_off[b];
+    k.cap = dst_cap[b];
+    k.P = 0;
+    k.staged = 0;
+    uint2* const gops = ops + (size_t)b * (kSlots * kOpMax);
+
+    // The exact decoder takes: destinations not 16-byte aligned, empty or huge
+    // blocks (lengths up to 255 * z must not wrap 32 bits).
+    bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
+    if (wave == 1) {
+        if (!refuse)
+            parser_wave<STAMPS>(S, k, gops, l, acc);
+        if (STAMPS && l == 0)
+            for (int i = 0; i < PH_N; i++)
+                if (parser_slot(i))
+                    stamps[(size_t)b * kStampSlots + i] = acc[i];
+        return;
+    }
+
+    uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t carry = 0;                        // output produced so far
+    uint32_t issued_seen = 0, landed_seen = 0; // last `issued` / `landed` read
+    uint32_t tag = 0;                          // step counter for the chunk tags
+    uint32_t q = 0, w0 = 0, total_ops = 0;     // piece, window start, piece's op count
+    bool have_piece = false, eofq = false;
+    uint64_t pf = 0;                           // prefetched op record of the next window
+    bool have_pf = false;
+
+    while (!refuse) {
+        if (!have_piece) {
+            // ---- the parser's piece q -------------------------------------------
+            for (uint32_t spin = 0; lds_load(&S.parsed) <= q; spin++) {
+                if (spin > (1u << 22)) {       // parser stuck: let the exact path redo it
+                    refuse = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (refuse)
+                break;
+            const uint32_t info = lds_load(&S.pinfo[q & (kSlots - 1)]);
+            STAMP(PH_EWAIT);
+            if (info & kInfoErr) {
                 refuse = true;
                 break;
             }
+            eofq = (info & kInfoEof) != 0;
+            total_ops = info & 0xFFFFu;
+            have_piece = true;
+            w0 = 0;
+            have_pf = false;
         }
+        if (w0 >= total_ops) {                 // piece done: its slot is free again
+            lds_store(&S.consumed, q + 1);
+            if (eofq)
+                break;                         // EOF consumed
 
-        // ---- execute the piece's ops, 64 at a time ----------------------------
-        for (uint32_t w0 = 0; w0 < total_ops && !refuse; w0 += kWave) {
+            q++;
+            have_piece = false;
+            continue;
+        }
+        const uint2* const slot = gops + (q & (kSlots - 1)) * kOpMax;
+        {
             const uint32_t nwin = total_ops - w0 < (uint32_t)kWave ? total_ops - w0 : (uint32_t)kWave;
             uint32_t L = 0, Sv = 0;
-            if (l < nwin) {
-                const uint32_t ref = S.opref[w0 + l];
-                const Step r = decode_step(S, k, k.P + (ref & 0x3FFu), (ref >> 10) & 3u);
-                const bool part = (ref >> 12) != 0;
-                L = part ? r.bL : r.aL;
-                Sv = part ? r.bS : r.aS;
+            {
+                // agent scope: served by L2, never by a stale L1 line of the slot's last use
+                uint64_t r = pf;
+                if (!have_pf && l < nwin)
+                    r = __hip_atomic_load((const uint64_t*)(slot + w0 + l), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                if (l < nwin) {
+                    L = (uint32_t)r;
+                    Sv = (uint32_t)(r >> 32);
+                }
             }
+            // what the source copy does not find in the ring (below carry -
+            // kRing) it reads from HBM: that output must have landed
+            if (carry > kRing)
+                landed_seen = wait_landed(S, carry - kRing, landed_seen, refuse);
+            if (refuse)
+                break;
+            // prefetch the next window's op records of this piece
+            have_pf = w0 + kWave < total_ops;
+            if (have_pf && w0 + kWave + l < total_ops)
+                pf = __hip_atomic_load((const uint64_t*)(slot + w0 + kWave + l), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
             STAMP(PH_WLOAD);
             if (STAMPS)
                 acc[CN_WINDOWS] += 1;
@@ -925,25 +1096,24 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             }
             // ---- op descriptors: byte x of op j reads
             //   src[b + ((x - o) mod p)]   (p == 0: src[b + x - o])
-            // in LDS at linear address b (kLitFlag set: the input staging or
-            // the far buffer; past the staging, the input in HBM) or in the
-            // output (ring / HBM).  A match starts as b = o - d, p = d if it
-            // overlaps itself (d < L).
-            uint32_t db = lit ? Sv + (kStageOff - k.P) : o - Sv;
+            // at linear address b (kLitFlag set: the LDS source buffer, or from
+            // kLinHbm the input in HBM) or in the output (ring / HBM).  A match
+            // starts as b = o - d, p = d if it overlaps itself (d < L).
+            const uint32_t ipos = Sv & ~kLitFlag;
+            uint32_t db = lit ? kLitFlag | (kLinHbm + ipos) : o - Sv;
             uint32_t dp = (!lit && Sv < L) ? Sv : 0u;
+            STAMP(PH_WSCAN);
+            const SrcCopy fc = src_issue(S, k, l, nwin, carry, landed_seen, o, L, dp, lit, ipos, db);
+            STAMP(PH_FARI);
+            if (STAMPS && fc.used)
+                acc[CN_SRCWIN] += 1;
+            if (STAMPS && fc.miss)
+                acc[CN_SRCMISS] += 1;
             // Source forwarding: a match whose source span lies inside one
             // earlier op of this window reads that op's source instead, so it
             // no longer waits for it.  Three parallel rounds reach the
             // sequential fixed point on ITB streams (600 -> 205 batches per
             // 64 KiB block).
-            STAMP(PH_WSCAN);
-            FarCopy fc;
-            fc.used = 0;
-            if (kFarDw)
-                fc = far_issue(S, k, l, nwin, carry, o, L, dp, db);
-            STAMP(PH_FARI);
-            if (STAMPS && fc.used)
-                acc[CN_FARWIN] += 1;
             const uint32_t o_first = lane_read(o, 0);
             for (int round = 0; round < POM_FWD_ROUNDS; round++) {
                 const uint32_t span = dp ? dp : L;
@@ -971,26 +1141,24 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     ok = r + span <= kp;
                 }
                 if (ok)
-                    db = kb + r;                       // (kb carries k's input flag)
+                    db = kb + r;                       // (kb carries k's linear flag)
             }
+            STAMP(PH_FWD);
+            src_commit(S, l, fc);
             // end of each output-sourced op's source span: a batch may not read
             // its own output
-            STAMP(PH_FWD);
-            if (kFarDw)
-                far_commit(S, l, fc);
             const bool outsrc = l < nwin && !(db & kLitFlag);
             const uint32_t span = dp ? dp : L;
             const uint32_t send = outsrc ? db + span : 0u;
             uint32_t inv = 0;                          // mod by mulhi; only overlapping matches
             if (wave_ballot(dp != 0))
                 inv = dp ? 0xFFFFFFFFu / dp : 0u;
-            // An op needs HBM reads if its literal source runs past the staging,
-            // or its output source may leave the ring before its last step
+            // An op needs HBM reads if its linear source is the input in HBM, or
+            // its output source may leave the ring before its last step
             // (sp + kRing < step start + 260 for some byte; far ops the buffer
             // did not take).
-            const uint32_t lin_end = kStageOff + k.staged;
             const bool gop = l < nwin && (outsrc ? db + kRing < o + (dp ? L : 0u) + 260u
-                                                 : (db & ~kLitFlag) + span > lin_end);
+                                                 : (db & ~kLitFlag) + span > kLinHbm);
             // Chunks: op j covers output chunks cs .. cs + ceil(L/4) - 1 of the
             // window, each up to 4 bytes of that op alone.
             const uint32_t nch = l < nwin ? (L + 3u) >> 2 : 0u;
@@ -1021,7 +1189,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     // chunk's slot; lane l's op is the last one started at or
                     // before chunk C + l (a ballot and mbcnt, no scan).
                     tag++;
-                    const uint32_t tagv = tag | 0x80000000u;   // far_issue's byte flags never set bit 31
+                    const uint32_t tagv = tag | 0x80000000u;   // src_issue's byte flags never set bit 31
                     if (starter && cs >= C && cs < C + kWave)
                         S.flags[cs - C] = tagv;
                     wave_order();
@@ -1044,15 +1212,16 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     const uint32_t xs = lane_read(x, 0);
                     const uint32_t step_end = lane_read(x + len, nl - 1);
                     STAMP(PH_FLAGS);
-                    // ring space: the slots of [xs, step_end) must be flushed
-                    // (and HBM reads below need flushed >= step_end - kRing + kRingSlack).
-                    for (uint32_t spin = 0; step_end > flushed_seen + kRing - kRingSlack; spin++) {
+                    // ring space: the stores of what the slots of [xs, step_end)
+                    // held must have been issued
+                    for (uint32_t spin = 0; step_end > issued_seen + kRing; spin++) {
                         if (spin > (1u << 22)) {       // writer stuck: let the exact path redo it
                             refuse = true;
                             break;
                         }
-                        __builtin_amdgcn_s_sleep(1);
-                        flushed_seen = lds_load(&S.flushed);
+                        if (spin)
+                            __builtin_amdgcn_s_sleep(1);
+                        issued_seen = lds_load(&S.issued);
                     }
                     if (refuse)
                         break;
@@ -1070,31 +1239,33 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                             r[i] = min(r[i - 1] + 1u, r[i - 1] + 1u - p);
                         const bool lin = (op.y & kLitFlag) != 0;
                         const uint32_t bb = live ? op.y & ~kLitFlag : 0u;
-                        // (linear sources past the staging read HBM below; masking
-                        // keeps their LDS read inside the allocation)
+                        // (linear sources in HBM read below; masking keeps their
+                        // LDS read inside the allocation)
                         const uint32_t amask = !live ? 0u : lin ? kLdsMask : kRingMask;
                         const uint8_t* lds = (const uint8_t*)&S;
                         uint32_t val = 0;
 #pragma unroll
                         for (uint32_t i = 0; i < 4; i++)
                             val |= (uint32_t)lds[(bb + r[i]) & amask] << (8 * i);
-                        if (gbatch) {                          // literal past staging / far match
+                        if (gbatch) {                          // literal in HBM / far match
                             const bool gj = (op.w & kLitFlag) != 0;
                             uint32_t gmask = 0;
 #pragma unroll
                             for (uint32_t i = 0; i < 4; i++) {
                                 const uint32_t sp = bb + r[i];
-                                const bool isg = gj && i < len && (lin ? sp >= lin_end : sp + kRing < xs + 260u);
+                                const bool isg = gj && i < len && (lin ? sp >= kLinHbm : sp + kRing < xs + 260u);
                                 gmask |= isg ? (1u << i) : 0u;
                             }
                             if (wave_ballot(gmask != 0)) {
-                                const uint32_t lin_in = kStageOff - k.P;     // LDS address - input position
+                                // output below xs + 260 - kRing is read from HBM
+                                if (xs + 260u > kRing)
+                                    landed_seen = wait_landed(S, xs + 260u - kRing, landed_seen, refuse);
                                 for (uint32_t i = 0; i < 4; i++) {
                                     if (!(gmask & (1u << i)))
                                         continue;
                                     const uint32_t sp = bb + r[i];
                                     const uint32_t bv = lin
-                                        ? (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + (sp - lin_in)))
+                                        ? (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + (sp - kLinHbm)))
                                         : global_byte_nt(k.out + sp);
                                     val = (val & ~(0xFFu << (8 * i))) | (bv << (8 * i));
                                 }
@@ -1117,13 +1288,13 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             carry += wtotal;
             wave_order();
         }
-        k.P += kPiece;
+        w0 += kWave;
     }
 
     if (STAMPS && l == 0)
         for (int i = 0; i < PH_N; i++)
-            stamps[(size_t)b * kStampSlots + i] = acc[i];
-#undef STAMP
+            if (!parser_slot(i))
+                stamps[(size_t)b * kStampSlots + i] = acc[i];
     if (l == 0) {
         if (refuse) {
             lds_store(&S.state, 2u);
@@ -1138,21 +1309,28 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         }
     }
 }
+#undef STAMP
 
 }  // namespace
+
+// Op slots per block in the decompression scratch (lzo_host.c sizes it).
+extern "C" size_t lzo_mi355x_fast_ops_bytes_per_block(void)
+{
+    return (size_t)kSlots * kOpMax * sizeof(uint2);
+}
 
 extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint64_t* src_off,
                                                  const uint32_t* src_len, uint8_t* dst,
                                                  const uint64_t* dst_off, const uint32_t* dst_cap,
                                                  uint32_t* out_len, int32_t* status,
-                                                 uint32_t* fallback, uint32_t nblocks,
+                                                 uint32_t* fallback, void* ops, uint32_t nblocks,
                                                  hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0,
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
-                       fallback, nblocks, nullptr);
+                       fallback, (uint2*)ops, nblocks, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1160,12 +1338,12 @@ extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint6
 extern "C" int lzo_mi355x_debug_decompress_fast_stamps(
     const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint8_t* dst,
     const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* out_len, int32_t* status,
-    uint32_t* fallback, uint32_t nblocks, uint64_t* stamps, hipStream_t stream)
+    uint32_t* fallback, void* ops, uint32_t nblocks, uint64_t* stamps, hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_fast_kernel<true>, dim3(nblocks), dim3(2 * kWave), 0,
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
-                       fallback, nblocks, stamps);
+                       fallback, (uint2*)ops, nblocks, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

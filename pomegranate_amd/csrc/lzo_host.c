@@ -158,9 +158,16 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                                       status, nblocks, 1, s);
 }
 
+/* Scratch: the fast decoder's fallback list [count, block ids], then its
+ * per-block op slots at a 256-byte boundary. */
+static size_t fallback_bytes(uint32_t nblocks)
+{
+    return (4 * ((size_t)nblocks + 1) + 255) & ~(size_t)255;
+}
+
 size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
 {
-    return 4 * ((size_t)nblocks + 1);
+    return fallback_bytes(nblocks) + (size_t)nblocks * lzo_mi355x_fast_ops_bytes_per_block();
 }
 
 /* Fast decoder over the whole batch, then the exact decoder over the blocks
@@ -182,7 +189,8 @@ int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
     if (hipMemsetAsync(fb, 0, 4, s) != hipSuccess)
         return -1;
     if (lzo_mi355x_launch_decompress_fast(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                          status, fb, nblocks, s) != 0)
+                                          status, fb, (uint8_t *)scratch + fallback_bytes(nblocks),
+                                          nblocks, s) != 0)
         return -1;
     const uint32_t ngrid = nblocks < 512 ? nblocks : 512;
     return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,

@@ -3,6 +3,7 @@
 #ifndef POM_LZO_MI355X_KERNELS_H
 #define POM_LZO_MI355X_KERNELS_H 1
 
+#include <stddef.h>
 #include <stdint.h>
 #include <hip/hip_runtime_api.h>
 
@@ -41,12 +42,15 @@ int lzo_mi355x_launch_decompress_exact(const uint8_t *src, const uint64_t *src_o
 
 /* Throughput decoder (lzo1x_decode_fast.hip).  Blocks it does not finish
  * exactly are appended to fb (fb[0] = count, must be 0 on entry) and get
- * status 0x7FFF0001 until the exact decoder runs on them. */
+ * status 0x7FFF0001 until the exact decoder runs on them.  ops: device
+ * scratch of nblocks * lzo_mi355x_fast_ops_bytes_per_block() bytes (the
+ * parser wave's op slots). */
+size_t lzo_mi355x_fast_ops_bytes_per_block(void);
 int lzo_mi355x_launch_decompress_fast(const uint8_t *src, const uint64_t *src_off,
                                       const uint32_t *src_len, uint8_t *dst,
                                       const uint64_t *dst_off, const uint32_t *dst_cap,
                                       uint32_t *out_len, int32_t *status, uint32_t *fb,
-                                      uint32_t nblocks, hipStream_t stream);
+                                      void *ops, uint32_t nblocks, hipStream_t stream);
 
 int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off,
                                      const uint32_t *src_len, uint32_t *out_len,

@@ -32,22 +32,24 @@ zsrc = lzo.DeviceBatch(za, zb.off, zl)
 out = torch.zeros_like(src.arena); ob = lzo.DeviceBatch(out, src.off, src.length)
 ol = torch.zeros_like(zl); os_ = torch.zeros_like(zl)
 fb = torch.zeros(nb + 1, dtype=torch.int32, device=dev)
+lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
+opsbuf = torch.empty(nb * lib.lzo_mi355x_fast_ops_bytes_per_block(), dtype=torch.uint8, device=dev)
 SLOTS = 32
 stamps = torch.zeros(nb * SLOTS, dtype=torch.int64, device=dev)
 fn = lib.lzo_mi355x_debug_decompress_fast_stamps
 fn.restype = ctypes.c_int
-fn.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+fn.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 fast = lib.lzo_mi355x_launch_decompress_fast
 fast.restype = ctypes.c_int
-fast.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_uint32, ctypes.c_void_p]
+fast.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
 p = lambda x: x.data_ptr()
 sh = torch.cuda.current_stream().cuda_stream
 def run(stamp):
     fb.zero_()
     if stamp:
-        fn(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), nb, p(stamps), sh)
+        fn(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), p(opsbuf), nb, p(stamps), sh)
     else:
-        fast(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), nb, sh)
+        fast(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), p(opsbuf), nb, sh)
 for stamp in (False, True):
     run(stamp); torch.cuda.synchronize()
     ts = []
@@ -59,14 +61,17 @@ for stamp in (False, True):
           f"fallback {int(fb[0].item())}, equal {torch.equal(out, src.arena)}")
 st = stamps.view(nb, SLOTS).double().cpu().numpy()
 # order of the kernel's PH_* / CN_* enum (lzo1x_decode_fast.hip)
-phases = ["stage", "pass1", "pwalk", "merge", "count", "write",
-          "wload", "wscan", "far_issue", "fwd", "far_commit+wop", "batch",
+phases = ["stage", "pass1", "pwalk", "merge", "count", "write", "p_slotwait", "p_duty",
+          "e_wait", "wload", "wscan", "src_issue", "fwd", "src_commit+wop", "batch",
           "space", "flags", "gather", "publish"]
-counts = ["walks", "windows", "far_windows", "batches", "steps",
-          "it_pass1", "it_pwalk", "it_walk", "it_count", "it_write", "fwd_rounds"]
-tot = st[:, :len(phases)].sum(1)
-print("cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases)},
-      "total", int(tot.mean()))
+counts = ["walks", "it_pass1", "it_pwalk", "it_walk", "it_count", "it_write", "pieces",
+          "windows", "src_windows", "src_miss", "batches", "steps", "fwd_rounds"]
+PARSER = 8   # phases [0, 8) belong to the parser wave, the rest to the executor
+ptot = st[:, :PARSER].sum(1); etot = st[:, PARSER:len(phases)].sum(1)
+print("parser cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases[:PARSER])},
+      "total", int(ptot.mean()))
+print("executor cycles/block (mean):", {n: int(st[:, PARSER + i].mean()) for i, n in enumerate(phases[PARSER:])},
+      "total", int(etot.mean()))
 print("counts/block (mean):", {n: round(float(st[:, len(phases) + i].mean()), 1)
                                for i, n in enumerate(counts)})
 print("zlen mean", float(zl.double().mean()))

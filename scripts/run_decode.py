@@ -12,7 +12,10 @@ ap.add_argument("--blocks", type=int, default=4096)
 ap.add_argument("--bytes", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--model", default="itb")
+ap.add_argument("--lib", default=None, help="alternative liblzo_mi355x.so build")
 a = ap.parse_args()
+if a.lib:
+    lzo.LIB_PATH = a.lib
 dev = torch.device("cuda:0"); torch.cuda.set_device(dev)
 model = {v: k for k, v in synth.MODEL_NAMES.items()}[a.model]
 arena, offs, lens = synth.batch(model, 0, [a.bytes] * a.blocks, threads=16)
