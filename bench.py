@@ -1,19 +1,27 @@
 #!/usr/bin/env python3
 """LZO1X block codec benchmark on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): 4096 x 64 KiB synthetic ITB blocks per
-GPU, LZO1X decompress-only, device-resident: inputs (the compressed blocks)
-and outputs live in HBM before the timed region starts.  A "step" is one
-decompression pass over the whole batch.  value = uncompressed GiB/s over
+Default workload (BASELINE.json configs[1], C2): 4096 x 64 KiB synthetic ITB
+blocks per GPU, LZO1X decompress-only, device-resident: inputs (the compressed
+blocks) and outputs live in HBM before the timed region starts.  A "step" is
+one decompression pass over the whole batch.  value = uncompressed GiB/s over
 all GPUs (sum of n over every rank / max-over-ranks time).
 
-Also reported (not the headline): LZO1X-1 compress GiB/s and compress +
-decompress round-trip GiB/s on the same blocks, the HBM roofline of the decode
-kernel, and the reference's own lib/minilzo.c (oracle/_ref, compiled from the
-reference sources) timed on this box's host cores on a bounded sample.
+Also reported on the default line (not the headline): LZO1X-1 compress GiB/s
+and compress + decompress round-trip GiB/s on the same blocks (C3), the HBM
+roofline of the decode kernel, and the reference's own lib/minilzo.c
+(oracle/_ref, compiled from the reference sources) timed on this box's host
+cores on a bounded sample -- whose compressed bytes are also compared with the
+GPU's (C3 byte identity).
+
+Other workloads (--workload):
+  c4  mixed 4-256 KiB ITB blocks, decompress GiB/s; --c4-blocks per GPU
+      (default 131072 = 1 M / 8: the 8-GPU run is exactly configs[3])
+  c5  end-to-end ITB write/read through the MDSL append-file loopback with
+      the host-resident batch API (pinned staging, hipMemcpyAsync in and out)
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): global
-block i goes to rank i mod N (weak scaling: 4096 blocks per GPU); the only
+block i goes to rank i mod N (weak scaling: per-GPU work fixed); the only
 collective is the RCCL completion barrier (error sum, elapsed max).
 """
 from __future__ import annotations
@@ -32,6 +40,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GIB = float(1 << 30)
+METRIC = "LZO1X compress+decompress GiB/s (device-resident), 4-256 KiB ITB block batches"
 
 
 def parse():
@@ -39,8 +48,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--blocks", type=int, default=4096, help="blocks per GPU")
+    p.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2")
+    p.add_argument("--blocks", type=int, default=4096, help="C2: blocks per GPU")
     p.add_argument("--block-bytes", type=int, default=65536)
+    p.add_argument("--c4-blocks", type=int, default=131072, help="C4: blocks per GPU")
+    p.add_argument("--c5-records", type=int, default=1024, help="C5: ITB records")
     p.add_argument("--model", default="itb")
     p.add_argument("--compress-steps", type=int, default=3)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -48,9 +60,14 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(arena, offs, lens, comps, seconds):
-    """Reference lib/minilzo.c (oracle/_ref) or, if absent, the oracle port,
-    on the host cores: decompress (and compress) of a bounded sample."""
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's lib/minilzo.c on the host cores
+# ---------------------------------------------------------------------------
+def cpu_baseline(plain, comps, seconds):
+    """Reference lib/minilzo.c (oracle/_ref) or, if absent, the oracle port, on
+    the host cores: decompress (and compress) of a bounded sample.  The
+    reference's compressed bytes of every sample block are compared with the
+    GPU's (C3 byte identity)."""
     from concurrent.futures import ThreadPoolExecutor
 
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libminilzo_ref.so")
@@ -74,43 +91,50 @@ def cpu_baseline(arena, offs, lens, comps, seconds):
         comp = None
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 16, os.cpu_count() or 1))
-    nsample = min(len(lens), 512)
+    nsample = len(plain)
+    lens = [len(p) for p in plain]
     srcs = [ctypes.create_string_buffer(comps[b], len(comps[b]) + 64) for b in range(nsample)]
-    plain = [arena[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes() for b in range(nsample)]
+
+    def compress_one(src, out, wrk):
+        ol = ulong(0)
+        if kind == "reference":
+            ctypes.memset(wrk, 0, 131072)
+            comp(src, len(src), out, ctypes.byref(ol), wrk)
+            return out.raw[: ol.value]
+        sz = ctypes.c_size_t(0)
+        lib.oracle_lzo1x_1_compress(src, ctypes.c_size_t(len(src)), out, ctypes.byref(sz))
+        return out.raw[: sz.value]
+
+    # C3: byte identity of the GPU's compressed blocks on the sample
+    out = ctypes.create_string_buffer(max(lens) * 2 + 128)
+    wrk = ctypes.create_string_buffer(131072)
+    identical = sum(compress_one(plain[b], out, wrk) == comps[b] for b in range(nsample))
 
     def dec_share(t, deadline, nbytes):
-        out = ctypes.create_string_buffer(int(max(lens)) + 64)
+        o = ctypes.create_string_buffer(max(lens) + 64)
         done = 0
         b = t
         while time.perf_counter() < deadline:
             ol = ulong(0)
             if kind == "reference":
-                rc = dec(srcs[b], len(comps[b]), out, ctypes.byref(ol), None)
+                rc = dec(srcs[b], len(comps[b]), o, ctypes.byref(ol), None)
             else:
-                sz = ctypes.c_size_t(len(out))
+                sz = ctypes.c_size_t(len(o))
                 rc = lib.oracle_lzo1x_decompress_safe(srcs[b], ctypes.c_size_t(len(comps[b])),
-                                                      out, ctypes.byref(sz))
+                                                      o, ctypes.byref(sz))
             assert rc == 0
-            done += int(lens[b])
+            done += lens[b]
             b = (b + threads) % nsample
         nbytes[t] = done
 
     def comp_share(t, deadline, nbytes):
-        out = ctypes.create_string_buffer(int(max(lens)) * 2 + 128)
-        wrk = ctypes.create_string_buffer(131072)
+        o = ctypes.create_string_buffer(max(lens) * 2 + 128)
+        w = ctypes.create_string_buffer(131072)
         done = 0
         b = t
         while time.perf_counter() < deadline:
-            ol = ulong(0)
-            src = plain[b]
-            if kind == "reference":
-                ctypes.memset(wrk, 0, 131072)
-                comp(src, len(src), out, ctypes.byref(ol), wrk)
-            else:
-                sz = ctypes.c_size_t(0)
-                lib.oracle_lzo1x_1_compress(src, ctypes.c_size_t(len(src)), out,
-                                            ctypes.byref(sz))
-            done += len(src)
+            compress_one(plain[b], o, w)
+            done += lens[b]
             b = (b + threads) % nsample
         nbytes[t] = done
 
@@ -125,7 +149,8 @@ def cpu_baseline(arena, offs, lens, comps, seconds):
         res[name] = sum(nbytes) / dt / GIB
     return {"value": round(res["decompress"], 4), "unit": "GiB/s", "cores": threads,
             "kind": kind, "compress_value": round(res["compress"], 4),
-            "sample": f"{nsample} of the same {int(lens[0])}-byte ITB blocks, round-robin over "
+            "byte_identical_blocks": f"{identical}/{nsample}",
+            "sample": f"{nsample} of the same {lens[0]}-byte ITB blocks, round-robin over "
                       f"{threads} threads for {seconds:.0f} s (decompress {0.6 * seconds:.0f} s,"
                       f" compress {0.4 * seconds:.0f} s), "
                       + ("lib/minilzo.c built from the reference sources (oracle/_ref)"
@@ -134,7 +159,8 @@ def cpu_baseline(arena, offs, lens, comps, seconds):
 
 def load_traffic(block_bytes, nblocks):
     """HBM bytes per decode launch from the committed rocprofv3 PMC summary,
-    when one exists for this workload (profiles/*decode_pmc.json)."""
+    when one exists for this workload (profiles/*decode_pmc.json; the newest
+    file name wins)."""
     import glob
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*decode_pmc.json"))):
@@ -146,6 +172,245 @@ def load_traffic(block_bytes, nblocks):
         if j.get("block_bytes") == block_bytes and j.get("nblocks") == nblocks:
             best = j
     return best
+
+
+# ---------------------------------------------------------------------------
+# Device-resident workloads (C2, C3, C4)
+# ---------------------------------------------------------------------------
+class Resident:
+    """Synthetic blocks in HBM, their GPU-compressed images, and output space."""
+
+    def __init__(self, torch, lzo, synth, dev, model, sizes, seeds, chunk=4096):
+        self.torch, self.lzo, self.dev = torch, lzo, dev
+        sizes = np.asarray(sizes, dtype=np.uint64)
+        nb = len(sizes)
+        pad = (sizes + np.uint64(255)) // np.uint64(256) * np.uint64(256)
+        offs = np.zeros(nb, dtype=np.uint64)
+        offs[1:] = np.cumsum(pad[:-1])
+        total = int(pad.sum())
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        arena = torch.empty(total, dtype=torch.uint8, device=dev)
+        for c0 in range(0, nb, chunk):             # generated on the host a chunk at a time
+            c1 = min(nb, c0 + chunk)
+            a, _, _ = synth.batch(model, 0, sizes[c0:c1], seeds=seeds[c0:c1], align=256,
+                                  threads=16)
+            base = int(offs[c0])
+            arena[base: base + a.size].copy_(torch.from_numpy(a))
+        self.n_bytes = float(sizes.astype(np.float64).sum())
+        self.sizes = sizes
+        self.src = lzo.DeviceBatch(arena, t(offs.view(np.int64)), t(sizes.astype(np.uint32).view(np.int32)))
+        caps = np.array([lzo.worst_compress(int(n)) for n in sizes], dtype=np.uint64)
+        zoffs = np.zeros(nb, dtype=np.uint64)
+        zoffs[1:] = np.cumsum((caps[:-1] + np.uint64(255)) // np.uint64(256) * np.uint64(256))
+        self.zoffs = zoffs
+        zarena = torch.empty(int(zoffs[-1] + caps[-1]) + 256, dtype=torch.uint8, device=dev)
+        self.zdst = lzo.DeviceBatch(zarena, t(zoffs.view(np.int64)),
+                                    t(caps.astype(np.uint32).view(np.int32)))
+        self.zlen = torch.zeros(nb, dtype=torch.int32, device=dev)
+        self.zst = torch.zeros(nb, dtype=torch.int32, device=dev)
+        self.out = torch.zeros_like(arena)
+        self.odst = lzo.DeviceBatch(self.out, self.src.off, self.src.length)
+        self.olen = torch.zeros(nb, dtype=torch.int32, device=dev)
+        self.ost = torch.zeros(nb, dtype=torch.int32, device=dev)
+        nscr = lzo.decompress_scratch_bytes(nb)
+        self.scratch = torch.empty(max(nscr, 1), dtype=torch.uint8, device=dev)
+        self.compress()
+        torch.cuda.synchronize()
+        self.zsrc = lzo.DeviceBatch(zarena, self.zdst.off, self.zlen)
+        self.decompress()
+        torch.cuda.synchronize()
+        self.z_bytes = float(self.zlen.double().sum().item())
+        self.fallback_blocks = int(self.scratch[:4].view(torch.int32).item())
+
+    def compress(self):
+        self.lzo.compress_dev(self.src, self.zdst, self.zlen, self.zst)
+
+    def decompress(self):
+        self.lzo.decompress_dev(self.zsrc, self.odst, self.olen, self.ost, self.scratch)
+
+    def errors(self):
+        torch = self.torch
+        e = int((self.zst != 0).sum().item()) + int((self.ost != 0).sum().item())
+        e += int((self.olen != self.src.length).sum().item())
+        return e + (0 if torch.equal(self.out, self.src.arena) else 1)
+
+    def sample(self, k):
+        """(plain, compressed) bytes of the first k blocks, for the CPU leg."""
+        zl = self.zlen[:k].cpu().numpy()
+        plain, comps = [], []
+        for b in range(k):
+            o, n = int(self.src.off[b].item()), int(self.sizes[b])
+            plain.append(self.src.arena[o: o + n].cpu().numpy().tobytes())
+            z0 = int(self.zoffs[b])
+            comps.append(self.zdst.arena[z0: z0 + int(zl[b])].cpu().numpy().tobytes())
+        return plain, comps
+
+
+def timed(torch, dist, world, stream, fn, steps, warmup):
+    """Wall time of `steps` calls (barrier + synchronize on both sides) and the
+    HIP-event time per call on the stream the kernels run on."""
+    for _ in range(warmup):
+        fn()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    return wall, ev0.elapsed_time(ev1) / 1e3 / max(steps, 1)
+
+
+def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend):
+    model = {v: k for k, v in synth.MODEL_NAMES.items()}[args.model]
+    if args.workload == "c2":
+        nglobal = args.blocks * world
+        mine = shard.round_robin(nglobal, rank, world)         # global ids i = rank mod G
+        sizes = [args.block_bytes] * len(mine)
+        workload = (f"configs[1]: {args.blocks} x {args.block_bytes // 1024} KiB {args.model} "
+                    "blocks per GPU, LZO1X decompress-only, device-resident")
+    else:
+        nglobal = args.c4_blocks * world
+        mine = shard.round_robin(nglobal, rank, world)
+        sizes = synth.mixed_sizes(nglobal, 4242)[mine]
+        workload = (f"configs[3]: {nglobal} mixed 4-256 KiB {args.model} blocks "
+                    f"round-robin over {world} GPU(s), LZO1X decompress-only, device-resident")
+    R = Resident(torch, lzo, synth, dev, model, sizes, np.asarray(mine, dtype=np.uint64))
+    stream = torch.cuda.current_stream()
+    errors = R.errors()
+    dec_wall, dec_kernel = timed(torch, dist, world, stream, R.decompress, args.steps,
+                                 args.warmup)
+    comp_wall, comp_kernel = timed(torch, dist, world, stream, R.compress,
+                                   args.compress_steps, 1)
+    errors += int((R.ost != 0).sum().item()) + int((R.zst != 0).sum().item())
+    n_bytes, z_bytes = R.n_bytes, R.z_bytes
+    if world > 1:
+        errors, dec_wall = shard.completion_barrier(dist, dev, errors, dec_wall)
+        _, comp_wall = shard.completion_barrier(dist, dev, 0, comp_wall)
+        tot = torch.tensor([n_bytes, z_bytes], dtype=torch.float64,
+                           device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(tot)
+        n_all, z_all = float(tot[0].item()), float(tot[1].item())
+    else:
+        n_all, z_all = n_bytes, z_bytes
+
+    value = n_all * args.steps / dec_wall / GIB
+    comp_gibps = n_all * args.compress_steps / comp_wall / GIB
+    rt_gibps = n_all / (dec_wall / args.steps + comp_wall / args.compress_steps) / GIB
+    achieved = (z_bytes + n_bytes) / dec_kernel / 1e9          # per GPU, decode launch
+    traffic = None
+    if args.workload == "c2":
+        rec = load_traffic(args.block_bytes, args.blocks)
+        traffic = rec.get("hbm_bytes_per_launch") if rec else None
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dec_wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic ITB payload images (SURVEY.md Appendix B generator, libpom_synth)",
+        "config": {"workload": workload, "blocks_per_gpu": len(mine),
+                   "block_bytes": args.block_bytes if args.workload == "c2" else "4-256 KiB",
+                   "compression_ratio": round(z_all / n_all, 4),
+                   "parallelism": f"round-robin blocks over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic,
+                     "kernel_ms": round(dec_kernel * 1e3, 4),
+                     "algorithmic_bytes_per_launch": int(z_bytes + n_bytes)},
+        "compress_gibps": round(comp_gibps, 3),
+        "roundtrip_gibps": round(rt_gibps, 3),
+        "compress_kernel_ms": round(comp_kernel * 1e3, 3),
+        "errors": errors,
+        "fallback_blocks": R.fallback_blocks,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c2":
+        plain, comps = R.sample(min(len(mine), 512))
+        result["cpu_baseline"] = cpu_baseline(plain, comps, args.cpu_seconds)
+    return result, errors
+
+
+# ---------------------------------------------------------------------------
+# C5: end-to-end ITB write/read with pinned host<->device copies
+# ---------------------------------------------------------------------------
+def run_c5(args, rank):
+    import tempfile
+
+    from pomegranate_amd import itb
+    rng = np.random.default_rng(5)
+    ites = rng.integers(1, 1025, args.c5_records)
+    recs = [itb.make_record(100000 + i, int(k)) for i, k in enumerate(ites)]
+    plain_bytes = float(sum(itb.header_fields(r)[0] - itb.ITBH_SIZE for r in recs))
+    originals = [bytes(r[: itb.header_fields(r)[0]]) for r in recs]
+    tmps = [bytearray(itb.ITB_FULL) for _ in recs]
+    itb.compress_batch(recs[:4], tmps[:4])                      # warm-up (context, staging)
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    path = os.path.join(d, f"pom_c5_{os.getpid()}_{rank}.itb")
+    res = {}
+    try:
+        best = None
+        for _ in range(max(1, args.steps // 5)):
+            t0 = time.perf_counter()
+            which, err = itb.compress_batch(recs, tmps)         # H2D + kernels + D2H
+            t1 = time.perf_counter()
+            af = itb.AppendFile(path)
+            locs = [af.append(o[: itb.header_fields(o)[0]])
+                    for o in (t if w else r for r, t, w in zip(recs, tmps, which))]
+            af.close()
+            t2 = time.perf_counter()
+            fd = os.open(path, os.O_RDONLY)
+            back = [itb.read_record(fd, loc) for loc in locs]
+            os.close(fd)
+            t3 = time.perf_counter()
+            comp_idx = [i for i, b in enumerate(back) if itb.header_fields(b)[2] == itb.COMPR_LZO]
+            derr, ok = itb.decompress_batch([back[i] for i in comp_idx])
+            t4 = time.perf_counter()
+            errors = sum(1 for e in err if e) + sum(1 for e in derr if e) + ok.count(0)
+            # the record as written, except h.zlen: itb_lzo_decompress leaves the
+            # uncompressed length there (mds/itb.c:2949-2980)
+            for b, o in zip(back, originals):
+                h = bytearray(b[: itb.ITBH_SIZE])
+                h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = o[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
+                errors += bytes(h) + bytes(b[itb.ITBH_SIZE: len(o)]) != o
+            cur = (t1 - t0, t2 - t0, t4 - t3, t4 - t2, errors, len(comp_idx),
+                   os.path.getsize(path))
+            if best is None or cur[1] + cur[3] < best[1] + best[3]:
+                best = cur
+        c, w, dcd, r, errors, ncomp, fbytes = best
+        res = {"records": len(recs), "uncompressed_bytes": int(plain_bytes),
+               "file_bytes": fbytes, "compressed_records": ncomp,
+               "write_gibps": round(plain_bytes / w / GIB, 3),
+               "read_gibps": round(plain_bytes / r / GIB, 3),
+               "compress_pcie_gibps": round(plain_bytes / c / GIB, 3),
+               "decompress_pcie_gibps": round(plain_bytes / dcd / GIB, 3),
+               "errors": errors}
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+    result = {
+        "metric": "LZO1X end-to-end ITB write/read GiB/s (host-resident, pinned copies)",
+        "value": res["read_gibps"], "unit": "GiB/s", "n_gpus": 1, "steps": max(1, args.steps // 5),
+        "warmup": 1, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic ITB records (real h.len distribution 12,416-536,192 B)",
+        "config": {"workload": "configs[4]: mdsl/storage.c ITB append-file write/read loopback "
+                               "(/dev/shm) with the GPU LZO drop-in, pinned host<->device copies "
+                               "included", "records": len(recs)},
+        "e2e": res,
+    }
+    return result, res["errors"]
 
 
 def main():
@@ -173,122 +438,11 @@ def main():
         else:
             dist.init_process_group(backend)
     lzo.load()
-
-    model = {v: k for k, v in synth.MODEL_NAMES.items()}[args.model]
-    nglobal = args.blocks * world
-    mine = shard.round_robin(nglobal, rank, world)       # global ids i = rank mod G
-    sizes = [args.block_bytes] * len(mine)
-    arena, offs, lens = synth.batch(model, 0, sizes, seeds=mine, threads=16)
-    nb = len(mine)
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    src = lzo.DeviceBatch(t(arena), t(offs.view(np.int64)), t(lens.view(np.int32)))
-    caps = np.array([lzo.worst_compress(int(n)) for n in lens], dtype=np.uint32)
-    zoffs = np.zeros(nb, dtype=np.uint64)
-    zoffs[1:] = np.cumsum((caps[:-1].astype(np.uint64) + 255) // 256 * 256)
-    zarena = torch.zeros(int(zoffs[-1]) + int(caps[-1]) + 256, dtype=torch.uint8, device=dev)
-    zdst = lzo.DeviceBatch(zarena, t(zoffs.view(np.int64)), t(caps.view(np.int32)))
-    zlen = torch.zeros(nb, dtype=torch.int32, device=dev)
-    zst = torch.zeros(nb, dtype=torch.int32, device=dev)
-    out = torch.zeros_like(src.arena)
-    odst = lzo.DeviceBatch(out, src.off, src.length)
-    olen = torch.zeros(nb, dtype=torch.int32, device=dev)
-    ost = torch.zeros(nb, dtype=torch.int32, device=dev)
-    nscr = lzo.decompress_scratch_bytes(nb)
-    scratch = torch.empty(max(nscr, 1), dtype=torch.uint8, device=dev) if nscr else None
-    stream = torch.cuda.current_stream()
-
-    # Compress on the GPU (also timed, secondary), check every block decodes back.
-    lzo.compress_dev(src, zdst, zlen, zst)
-    torch.cuda.synchronize()
-    zsrc = lzo.DeviceBatch(zarena, zdst.off, zlen)
-    lzo.decompress_dev(zsrc, odst, olen, ost, scratch)
-    torch.cuda.synchronize()
-    fallback_blocks = int(scratch[:4].view(torch.int32).item()) if scratch is not None else nb
-    errors = int((zst != 0).sum().item()) + int((ost != 0).sum().item())
-    errors += int((olen != src.length).sum().item()) + (0 if torch.equal(out, src.arena) else 1)
-    n_bytes = float(lens.astype(np.float64).sum())
-    z_bytes = float(zlen.double().sum().item())
-
-    def timed(fn, steps, warmup):
-        for _ in range(warmup):
-            fn()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for _ in range(steps):
-            fn()
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        wall = time.perf_counter() - t0
-        return wall, ev0.elapsed_time(ev1) / 1e3 / max(steps, 1)
-
-    dec_wall, dec_kernel = timed(lambda: lzo.decompress_dev(zsrc, odst, olen, ost, scratch),
-                                 args.steps, args.warmup)
-    comp_wall, comp_kernel = timed(lambda: lzo.compress_dev(src, zdst, zlen, zst),
-                                   args.compress_steps, 1)
-    errors += int((ost != 0).sum().item()) + int((zst != 0).sum().item())
-
-    if world > 1:
-        errors, dec_wall = shard.completion_barrier(dist, dev, errors, dec_wall)
-        _, comp_wall = shard.completion_barrier(dist, dev, 0, comp_wall)
-        tot = torch.tensor([n_bytes, z_bytes], dtype=torch.float64,
-                           device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(tot)
-        n_all, z_all = float(tot[0].item()), float(tot[1].item())
+    if args.workload == "c5":
+        result, errors = run_c5(args, rank)
     else:
-        n_all, z_all = n_bytes, z_bytes
-
-    ms_per_step = dec_wall / args.steps * 1e3
-    value = n_all * args.steps / dec_wall / GIB
-    comp_gibps = n_all * args.compress_steps / comp_wall / GIB
-    rt_gibps = n_all / (dec_wall / args.steps + comp_wall / args.compress_steps) / GIB
-    achieved = (z_bytes + n_bytes) / dec_kernel / 1e9      # per GPU, decode kernel
-    traffic_rec = load_traffic(args.block_bytes, args.blocks)
-    traffic = traffic_rec.get("hbm_bytes_per_launch") if traffic_rec else None
-
-    result = {
-        "metric": "LZO1X compress+decompress GiB/s (device-resident), 4-256 KiB ITB block batches",
-        "value": round(value, 3),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic ITB payload images (SURVEY.md Appendix B generator, libpom_synth)",
-        "config": {"workload": f"configs[1]: {args.blocks} x {args.block_bytes // 1024} KiB "
-                               f"{args.model} blocks per GPU, LZO1X decompress-only, "
-                               "device-resident",
-                   "blocks_per_gpu": args.blocks, "block_bytes": args.block_bytes,
-                   "compression_ratio": round(z_all / n_all, 4),
-                   "parallelism": f"round-robin blocks over {world} GPU(s)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic,
-                     "kernel_ms": round(dec_kernel * 1e3, 4),
-                     "algorithmic_bytes_per_launch": int(z_bytes + n_bytes)},
-        "compress_gibps": round(comp_gibps, 3),
-        "roundtrip_gibps": round(rt_gibps, 3),
-        "compress_kernel_ms": round(comp_kernel * 1e3, 3),
-        "errors": errors,
-        "fallback_blocks": fallback_blocks,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu:
-        lens_np = np.asarray(lens)
-        zl = zlen.cpu().numpy()
-        zh = zarena.cpu().numpy()
-        zo = zoffs
-        comps = [zh[int(zo[b]): int(zo[b]) + int(zl[b])].tobytes() for b in range(min(nb, 512))]
-        result["cpu_baseline"] = cpu_baseline(arena, offs, lens_np, comps, args.cpu_seconds)
+        result, errors = run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank,
+                                      backend)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

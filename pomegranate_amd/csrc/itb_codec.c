@@ -1,0 +1,270 @@
+/*
+ * itb_codec.c -- ITB record codec and MDSL append-file loopback over the
+ * host-resident LZO1X batch API (include/pom_itb.h).
+ *
+ * The per-record semantics follow the reference one for one:
+ *   compress   mds/itb.c:2904-2945  (header copy, incompressible fallback,
+ *                                    len/zlen swap, COMPR_LZO)
+ *   decompress mds/itb.c:2949-2980, mdsl/gc.c:755-786 (payload copied aside,
+ *                                    decoded in place, COMPR_NONE, len back)
+ *   append     mdsl/storage.c:455-519 (append_buf_write), :384-451
+ *              (append_buf_flush_remap)
+ * The LZO work of a whole batch is one GPU round trip (lzo_host.c).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include "lzo_mi355x.h"
+#include "minilzo.h"
+#include "pom_itb.h"
+
+static uint32_t rd32(const uint8_t *p)
+{
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v;
+}
+
+static void wr32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
+static void wr16(uint8_t *p, uint16_t v) { memcpy(p, &v, 2); }
+
+int pom_itb_lzo_compress_batch(uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
+                               uint8_t **oi, int *err, size_t n)
+{
+    if (n == 0)
+        return LZO_E_OK;
+    const uint8_t **src = malloc(n * sizeof(*src));
+    uint8_t **dst = malloc(n * sizeof(*dst));
+    uint8_t **aside = calloc(n, sizeof(*aside));   /* when tmp cannot take the worst case */
+    size_t *slen = malloc(n * sizeof(*slen));
+    size_t *dlen = malloc(n * sizeof(*dlen));
+    int *st = malloc(n * sizeof(*st));
+    int rc = LZO_E_OUT_OF_MEMORY;
+    if (!src || !dst || !aside || !slen || !dlen || !st)
+        goto out;
+    for (size_t b = 0; b < n; b++) {
+        oi[b] = in[b];
+        const uint32_t len = rd32(in[b] + POM_ITBH_LEN_OFF);
+        slen[b] = len >= POM_ITBH_SIZE ? len - POM_ITBH_SIZE : 0;
+        src[b] = in[b] + POM_ITBH_SIZE;
+        dst[b] = tmp[b] + POM_ITBH_SIZE;
+        const size_t worst = lzo_mi355x_worst_compress(slen[b]);
+        if (tmp_cap[b] < POM_ITBH_SIZE + worst) {
+            aside[b] = malloc(worst);
+            if (!aside[b])
+                goto out;
+            dst[b] = aside[b];
+        }
+        err[b] = len >= POM_ITBH_SIZE ? 0 : -EINVAL;
+    }
+    rc = lzo_mi355x_compress_batch(src, slen, dst, dlen, st, n);
+    if (rc != LZO_E_OK)
+        goto out;
+    for (size_t b = 0; b < n; b++) {
+        if (err[b])
+            continue;
+        memcpy(tmp[b], in[b], POM_ITBH_SIZE);                  /* the itb header */
+        if (st[b] != LZO_E_OK) {
+            err[b] = st[b];
+            continue;
+        }
+        if (dlen[b] >= slen[b])                                /* impossible to compress */
+            continue;
+        if (aside[b])
+            memcpy(tmp[b] + POM_ITBH_SIZE, aside[b], dlen[b]);
+        wr32(tmp[b] + POM_ITBH_ZLEN_OFF, rd32(tmp[b] + POM_ITBH_LEN_OFF));
+        wr32(tmp[b] + POM_ITBH_LEN_OFF, (uint32_t)(POM_ITBH_SIZE + dlen[b]));
+        wr16(tmp[b] + POM_ITBH_ALGO_OFF, POM_COMPR_LZO);
+        oi[b] = tmp[b];
+    }
+out:
+    if (aside)
+        for (size_t b = 0; b < n; b++)
+            free(aside[b]);
+    free(aside);
+    free(src);
+    free(dst);
+    free(slen);
+    free(dlen);
+    free(st);
+    return rc;
+}
+
+int pom_itb_lzo_decompress_batch(uint8_t *const *in, const size_t *cap, int *err,
+                                 int *len_ok, size_t n)
+{
+    if (n == 0)
+        return LZO_E_OK;
+    const uint8_t **src = malloc(n * sizeof(*src));
+    uint8_t **dst = malloc(n * sizeof(*dst));
+    size_t *slen = malloc(n * sizeof(*slen));
+    size_t *dlen = malloc(n * sizeof(*dlen));
+    size_t *off = malloc(n * sizeof(*off));
+    int *st = malloc(n * sizeof(*st));
+    uint8_t *copy = NULL;
+    int rc = LZO_E_OUT_OF_MEMORY;
+    if (!src || !dst || !slen || !dlen || !off || !st)
+        goto out;
+    size_t total = 0;
+    for (size_t b = 0; b < n; b++) {
+        const uint32_t len = rd32(in[b] + POM_ITBH_LEN_OFF);
+        slen[b] = len >= POM_ITBH_SIZE ? len - POM_ITBH_SIZE : 0;
+        off[b] = total;
+        total += slen[b];
+    }
+    /* the payloads are copied aside: the output overwrites them in place */
+    copy = malloc(total ? total : 1);
+    if (!copy)
+        goto out;
+    for (size_t b = 0; b < n; b++) {
+        memcpy(copy + off[b], in[b] + POM_ITBH_SIZE, slen[b]);
+        src[b] = copy + off[b];
+        dst[b] = in[b] + POM_ITBH_SIZE;
+        dlen[b] = cap[b] > POM_ITBH_SIZE ? cap[b] - POM_ITBH_SIZE : 0;
+    }
+    rc = lzo_mi355x_decompress_batch(src, slen, dst, dlen, st, n);
+    if (rc != LZO_E_OK)
+        goto out;
+    for (size_t b = 0; b < n; b++) {
+        const uint32_t zlen = rd32(in[b] + POM_ITBH_ZLEN_OFF);
+        err[b] = st[b];
+        if (len_ok)
+            len_ok[b] = st[b] == LZO_E_OK && dlen[b] + POM_ITBH_SIZE == zlen;
+        wr16(in[b] + POM_ITBH_ALGO_OFF, POM_COMPR_NONE);       /* clear the compress flag */
+        wr32(in[b] + POM_ITBH_LEN_OFF, (uint32_t)(dlen[b] + POM_ITBH_SIZE));
+    }
+out:
+    free(copy);
+    free(src);
+    free(dst);
+    free(slen);
+    free(dlen);
+    free(off);
+    free(st);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* MDSL append buffer                                                       */
+/* ------------------------------------------------------------------------ */
+static int abuf_map(struct pom_abuf *ab)
+{
+    if (ab->file_offset + ab->win > ab->falloc_end) {
+        /* reserve two windows ahead (mdsl/storage.c:419-430) */
+        const uint64_t end = ab->file_offset + 2 * (uint64_t)ab->win;
+        if (ftruncate(ab->fd, (off_t)end) != 0)
+            return -errno;
+        ab->falloc_end = end;
+    }
+    void *a = mmap(NULL, ab->win, PROT_READ | PROT_WRITE, MAP_SHARED, ab->fd,
+                   (off_t)ab->file_offset);
+    if (a == MAP_FAILED)
+        return -errno;
+    ab->addr = a;
+    ab->offset = 0;
+    return 0;
+}
+
+int pom_abuf_open(struct pom_abuf *ab, const char *path, size_t win)
+{
+    const size_t page = (size_t)sysconf(_SC_PAGESIZE);
+    memset(ab, 0, sizeof(*ab));
+    ab->fd = -1;
+    if (win == 0)
+        win = 64u << 20;
+    ab->win = (win + page - 1) / page * page;
+    ab->fd = open(path, O_RDWR | O_CREAT | O_TRUNC, 0644);
+    if (ab->fd < 0)
+        return -errno;
+    const int rc = abuf_map(ab);
+    if (rc) {
+        close(ab->fd);
+        ab->fd = -1;
+    }
+    return rc;
+}
+
+int pom_abuf_append(struct pom_abuf *ab, const void *rec, size_t len, uint64_t *location)
+{
+    if (!ab->addr || !rec)
+        return -EINVAL;
+    const uint8_t *p = rec;
+    size_t done = 0;
+    if (location)
+        *location = ab->file_offset + ab->offset;
+    while (done < len) {
+        size_t w = ab->win - ab->offset;
+        if (w > len - done)
+            w = len - done;
+        memcpy(ab->addr + ab->offset, p + done, w);
+        done += w;
+        ab->offset += w;
+        if (ab->offset >= ab->win) {
+            /* flush + remap the next window (mdsl/storage.c:384-451) */
+            if (munmap(ab->addr, ab->win) != 0)
+                return -errno;
+            ab->addr = NULL;
+            ab->file_offset += ab->win;
+            const int rc = abuf_map(ab);
+            if (rc)
+                return rc;
+        }
+    }
+    ab->acclen += len;
+    return 0;
+}
+
+int pom_abuf_close(struct pom_abuf *ab)
+{
+    int rc = 0;
+    if (ab->addr && munmap(ab->addr, ab->win) != 0)
+        rc = -errno;
+    ab->addr = NULL;
+    if (ab->fd >= 0) {
+        if (ftruncate(ab->fd, (off_t)(ab->file_offset + ab->offset)) != 0 && !rc)
+            rc = -errno;
+        if (close(ab->fd) != 0 && !rc)
+            rc = -errno;
+    }
+    ab->fd = -1;
+    return rc;
+}
+
+static int pread_full(int fd, uint8_t *buf, size_t len, uint64_t off)
+{
+    size_t done = 0;
+    while (done < len) {
+        const ssize_t r = pread(fd, buf + done, len - done, (off_t)(off + done));
+        if (r < 0) {
+            if (errno == EINTR)
+                continue;
+            return -errno;
+        }
+        if (r == 0)
+            return -EIO;
+        done += (size_t)r;
+    }
+    return 0;
+}
+
+int pom_itb_read(int fd, uint64_t location, uint8_t *buf, size_t cap, size_t *len)
+{
+    if (cap < POM_ITBH_SIZE)
+        return -EINVAL;
+    int rc = pread_full(fd, buf, POM_ITBH_SIZE, location);            /* the header first */
+    if (rc)
+        return rc;
+    const uint32_t l = rd32(buf + POM_ITBH_LEN_OFF);
+    if (l < POM_ITBH_SIZE || l > cap)
+        return -EINVAL;
+    rc = pread_full(fd, buf + POM_ITBH_SIZE, l - POM_ITBH_SIZE, location + POM_ITBH_SIZE);
+    if (rc)
+        return rc;
+    *len = l;
+    return 0;
+}

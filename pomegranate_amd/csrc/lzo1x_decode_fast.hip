@@ -53,7 +53,11 @@ constexpr uint32_t kSeg = POM_SEG;               // input bytes per lane per pie
 constexpr uint32_t kLook = POM_LOOK;             // speculative lead-in before a segment
 constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
 constexpr uint32_t kStageBytes = kPiece + 512;
-constexpr uint32_t kOpMax = 32 * kSeg;           // ops per piece
+// Ops per piece: an instruction that yields two ops (a match and its 1-3
+// trailing literals) is at least 3 bytes, so a piece holds at most
+// ceil(kPiece / 3) * 2 ops (683 for 1 KiB).
+constexpr uint32_t kOpMax = (kPiece + 2) / 3 * 2 + 64;
+static_assert(kOpMax < (1u << 16), "piece info: 16-bit op count");
 #ifndef POM_SLOTS
 #define POM_SLOTS 4
 #endif
@@ -88,6 +92,9 @@ constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wra
 constexpr int32_t kFallback = 0x7FFF0001;        // status: exact decoder pending
 constexpr uint32_t kInfoEof = 1u << 16;          // piece info: the piece ends with EOF
 constexpr uint32_t kInfoErr = 1u << 17;          // piece info: the block needs the exact decoder
+// (diagnostics: why, in bits 20..23 of the piece info / the CN_REASON stamp)
+enum { RS_NONE, RS_OFF_END, RS_BAD, RS_OPS, RS_DEAD, RS_EWAIT, RS_OVERRUN, RS_LOOKBEHIND,
+       RS_SPACE, RS_LANDED, RS_HEAD };
 
 // parse states (instruction starts)
 constexpr uint32_t ST_A = 0;   // top: t < 16 is a literal run
@@ -95,6 +102,7 @@ constexpr uint32_t ST_B = 1;   // after a literal run: t < 16 is a 3-byte M1 (di
 constexpr uint32_t ST_C = 2;   // after trailing literals: t < 16 is a 2-byte M1
 constexpr uint32_t ST_F = 3;   // first byte of the stream (lib/minilzo.c:3357)
 constexpr uint32_t kPosEnd = 0xFFFFFFF0u;        // exit marker: EOF reached / dead path
+constexpr uint32_t kGenMax = 31;                 // restart generations a mark can tell apart
 constexpr uint32_t kPosUnknown = 0xFFFFFFE0u;    // speculative walk gave up
 
 struct __attribute__((aligned(16))) FastLds {
@@ -454,7 +462,7 @@ __device__ __forceinline__ uint32_t walk_uniform(const FastLds& S, const Blk& k,
             st = 0;
             return steps;
         }
-        if (pos >= c0 && S.marks[pos - k.P] == ((st + 1) | (gen << 2))) {
+        if (pos >= c0 && S.marks[pos - k.P] == ((st + 1) | (gen << 3))) {
             pos = xpos;
             st = xst;
             return steps;
@@ -486,8 +494,9 @@ enum { PH_STAGE, PH_PASS1, PH_PWALK, PH_MERGE, PH_COUNT, PH_WRITE, PH_PSLOT, PH_
        PH_SPACE, PH_FLAGS, PH_GATHER, PH_PUB,
        CN_FIRST, CN_WALKS = CN_FIRST, CN_IT_PASS1, CN_IT_PWALK, CN_IT_WALK, CN_IT_COUNT,
        CN_IT_WRITE, CN_PIECES,
-       CN_WINDOWS, CN_SRCWIN, CN_SRCMISS, CN_BATCHES, CN_STEPS, CN_FWD_ROUNDS, PH_N };
-constexpr int kStampSlots = 32;
+       CN_WINDOWS, CN_SRCWIN, CN_SRCMISS, CN_BATCHES, CN_STEPS, CN_FWD_ROUNDS,
+       CN_REASON, PH_N };
+constexpr int kStampSlots = 40;
 static_assert(PH_N <= kStampSlots, "stamp slots per block");
 __device__ __forceinline__ bool parser_slot(int i)
 {
@@ -583,6 +592,7 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
             acc[CN_PIECES] += 1;
         uint2* const slot = gops + (q & (kSlots - 1)) * kOpMax;
         bool err = k.P >= k.z;                 // ran off the end without EOF
+        uint32_t reason = err ? (uint32_t)RS_OFF_END : (uint32_t)RS_NONE;
         bool eof = false;
         uint32_t total_ops = 0;
         uint32_t next_pos = 0, next_st = 0;
@@ -608,9 +618,10 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
             const uint32_t c1 = c0 + kSeg;
 
             // ---- pass 1: speculative walk, mark visited points ---------------
-            // A mark is (state + 1) | (gen << 2); gen counts this lane's
-            // restarts, and only marks of the final generation lie on the path
-            // that really reaches xpos (a restart breaks the chain).
+            // A mark is (state + 1) | (gen << 3) -- state + 1 takes 3 bits, ST_F
+            // included; gen counts this lane's restarts, and only marks of the
+            // final generation lie on the path that really reaches xpos (a
+            // restart breaks the chain).
             const bool p1 = c1 > entry_pos;            // else no instruction starts here
             uint32_t pos = c0 >= k.P + kLook ? c0 - kLook : k.P;
             if (pos < entry_pos)
@@ -623,13 +634,13 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
                     break;
                 if (act) {
                     if (pos >= c0)
-                        S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 2));
+                        S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 3));
                     bool slow = false;
                     const Step r = decode_step<true>(S, k, pos, st, &slow);
                     if (r.bad || r.eof) {              // impossible guess: restart later
                         pos++;
                         st = ST_A;
-                        gen = gen < 63 ? gen + 1 : 63;
+                        gen = gen < kGenMax ? gen + 1 : kGenMax;
                     } else {
                         pos = r.pos;
                         st = r.st;
@@ -646,7 +657,7 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
             }
             const uint32_t xpos = !p1 ? entry_pos : pos >= k.z ? kPosEnd : pos;
             const uint32_t xst = !p1 ? entry_st : st;
-            const uint32_t xgen = !p1 ? 0u : gen < 63 ? gen : 0xFFu;   // saturated: never merge
+            const uint32_t xgen = !p1 ? 0u : gen < kGenMax ? gen : 0xFFu;   // saturated: never merge
             wave_order();
             STAMP(PH_PASS1);
 
@@ -752,6 +763,8 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
             const uint32_t incl = wave_incl_scan(nops);
             total_ops = lane_read(incl, kWave - 1);
             err = wave_ballot(lane_err) != 0 || total_ops > kOpMax;
+            if (err)
+                reason = wave_ballot(lane_err) != 0 ? RS_BAD : RS_OPS;
             eof = wave_ballot(lane_eof) != 0;
             STAMP(PH_COUNT);
             if (writer_duty(S, k.out, l, w) == 2)
@@ -777,14 +790,16 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
                 if (STAMPS)
                     acc[CN_IT_WRITE] += wave_max_dbg(itw);
             }
-            if (!eof && next_pos == kPosEnd)
+            if (!err && !eof && next_pos == kPosEnd) {
                 err = true;                            // dead without EOF
+                reason = RS_DEAD;
+            }
             STAMP(PH_WRITE);
         }
         // publish piece q once its op records landed
         __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
         lds_store(&S.pinfo[q & (kSlots - 1)],
-                  total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u));
+                  total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u) | (reason << 20));
         lds_store(&S.parsed, q + 1);
         STAMP(PH_WRITE);
         if (err || eof)
@@ -1000,6 +1015,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     // The exact decoder takes: destinations not 16-byte aligned, empty or huge
     // blocks (lengths up to 255 * z must not wrap 32 bits).
     bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
+    uint32_t reason = refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
     if (wave == 1) {
         if (!refuse)
             parser_wave<STAMPS>(S, k, gops, l, acc);
@@ -1025,6 +1041,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             for (uint32_t spin = 0; lds_load(&S.parsed) <= q; spin++) {
                 if (spin > (1u << 22)) {       // parser stuck: let the exact path redo it
                     refuse = true;
+                    reason = RS_EWAIT;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -1035,10 +1052,15 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             STAMP(PH_EWAIT);
             if (info & kInfoErr) {
                 refuse = true;
+                reason = (info >> 20) & 15u;
                 break;
             }
             eofq = (info & kInfoEof) != 0;
             total_ops = info & 0xFFFFu;
+#ifdef POM_EXEC_SKIP
+            if (POM_EXEC_SKIP)                 // (timing experiment only: parser alone)
+                total_ops = 0;
+#endif
             have_piece = true;
             w0 = 0;
             have_pf = false;
@@ -1071,8 +1093,10 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             // kRing) it reads from HBM: that output must have landed
             if (carry > kRing)
                 landed_seen = wait_landed(S, carry - kRing, landed_seen, refuse);
-            if (refuse)
+            if (refuse) {
+                reason = RS_LANDED;
                 break;
+            }
             // prefetch the next window's op records of this piece
             have_pf = w0 + kWave < total_ops;
             if (have_pf && w0 + kWave + l < total_ops)
@@ -1086,12 +1110,14 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             const uint32_t wtotal = lane_read(inc, kWave - 1);
             if (carry + wtotal < carry || carry + wtotal > k.cap) {
                 refuse = true;                         // OUTPUT_OVERRUN (or wrap)
+                reason = RS_OVERRUN;
                 break;
             }
             const bool lit = (Sv & kLitFlag) != 0;
             const bool lb = l < nwin && !lit && Sv > o;     // LOOKBEHIND_OVERRUN
             if (wave_ballot(lb)) {
                 refuse = true;
+                reason = RS_LOOKBEHIND;
                 break;
             }
             // ---- op descriptors: byte x of op j reads
@@ -1217,6 +1243,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     for (uint32_t spin = 0; step_end > issued_seen + kRing; spin++) {
                         if (spin > (1u << 22)) {       // writer stuck: let the exact path redo it
                             refuse = true;
+                            reason = RS_SPACE;
                             break;
                         }
                         if (spin)
@@ -1291,6 +1318,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         w0 += kWave;
     }
 
+    if (STAMPS)
+        acc[CN_REASON] = reason | (q << 4) | ((uint64_t)w0 << 32);
     if (STAMPS && l == 0)
         for (int i = 0; i < PH_N; i++)
             if (!parser_slot(i))

@@ -45,6 +45,9 @@ EXPORTS = (
     "lzo_mi355x_compress_dev", "lzo_mi355x_decompress_dev",
     "lzo_mi355x_decompress_scratch", "lzo_mi355x_decoded_length_dev",
     "lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
+    # include/pom_itb.h
+    "pom_itb_lzo_compress_batch", "pom_itb_lzo_decompress_batch",
+    "pom_abuf_open", "pom_abuf_append", "pom_abuf_close", "pom_itb_read",
 )
 
 _lib: Optional[ctypes.CDLL] = None

@@ -34,7 +34,7 @@ ol = torch.zeros_like(zl); os_ = torch.zeros_like(zl)
 fb = torch.zeros(nb + 1, dtype=torch.int32, device=dev)
 lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
 opsbuf = torch.empty(nb * lib.lzo_mi355x_fast_ops_bytes_per_block(), dtype=torch.uint8, device=dev)
-SLOTS = 32
+SLOTS = 40
 stamps = torch.zeros(nb * SLOTS, dtype=torch.int64, device=dev)
 fn = lib.lzo_mi355x_debug_decompress_fast_stamps
 fn.restype = ctypes.c_int
@@ -65,7 +65,7 @@ phases = ["stage", "pass1", "pwalk", "merge", "count", "write", "p_slotwait", "p
           "e_wait", "wload", "wscan", "src_issue", "fwd", "src_commit+wop", "batch",
           "space", "flags", "gather", "publish"]
 counts = ["walks", "it_pass1", "it_pwalk", "it_walk", "it_count", "it_write", "pieces",
-          "windows", "src_windows", "src_miss", "batches", "steps", "fwd_rounds"]
+          "windows", "src_windows", "src_miss", "batches", "steps", "fwd_rounds", "reason"]
 PARSER = 8   # phases [0, 8) belong to the parser wave, the rest to the executor
 ptot = st[:, :PARSER].sum(1); etot = st[:, PARSER:len(phases)].sum(1)
 print("parser cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases[:PARSER])},
@@ -75,3 +75,15 @@ print("executor cycles/block (mean):", {n: int(st[:, PARSER + i].mean()) for i, 
 print("counts/block (mean):", {n: round(float(st[:, len(phases) + i].mean()), 1)
                                for i, n in enumerate(counts)})
 print("zlen mean", float(zl.double().mean()))
+rsf = stamps.view(nb, SLOTS)[:, len(phases) + counts.index("reason")].cpu().numpy()
+rs = (rsf & 15).astype(int)
+for b in np.nonzero(rs)[0][:4]:
+    q, w0 = int((rsf[b] >> 4) & 0xFFFFFFF), int(rsf[b] >> 32)
+    per = opsbuf.numel() // nb
+    slot = opsbuf[b * per: (b + 1) * per].view(torch.int32).view(-1, 2).cpu().numpy()
+    kslots = 4
+    ops_q = slot[(q % kslots) * (len(slot) // kslots): (q % kslots + 1) * (len(slot) // kslots)]
+    np.save(os.path.join(ROOT, "gpurun_out", f"refused_b{b}_q{q}.npy"), ops_q)
+    print("refused block", int(b), "reason", int(rs[b]), "piece", q, "window", w0)
+names = ["none", "off_end", "bad", "ops", "dead", "ewait", "overrun", "lookbehind", "space", "landed", "head"]
+print("refusals:", {names[r]: int((rs == r).sum()) for r in np.unique(rs) if r})

@@ -65,6 +65,21 @@ def gpu_decompress(torch, comps: Sequence[bytes], caps: Sequence[int], dev, shif
     return outs, st.cpu().numpy().tolist(), dst
 
 
+def gpu_decompress_fast(torch, comps: Sequence[bytes], caps: Sequence[int], dev):
+    """gpu_decompress plus the number of blocks the throughput decoder handed
+    to the exact decoder (the fallback list count at the head of scratch)."""
+    src = device_batch(torch, comps, dev)
+    dst = empty_batch(torch, caps, dev, fill=0x5A)
+    n = len(comps)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    scratch = torch.zeros(lzo.decompress_scratch_bytes(n), dtype=torch.uint8, device=dev)
+    lzo.decompress_dev(src, dst, olen, st, scratch)
+    torch.cuda.synchronize()
+    fallbacks = int(scratch[:4].view(torch.int32).item())
+    return fetch(dst, olen, cap=caps), st.cpu().numpy().tolist(), fallbacks
+
+
 def fetch(batch, olen, cap=None) -> List[bytes]:
     host = batch.arena.cpu().numpy()
     off = batch.off.cpu().numpy()

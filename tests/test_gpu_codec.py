@@ -176,3 +176,38 @@ def test_encoder_adversarial_vs_oracle(dev, gu, oracle):
         assert c == oracle.compress(b), (i, len(b))
     outs, st2, _ = gu.gpu_decompress(torch, comps, [len(b) for b in blocks], dev, shift=1)
     assert all(s == 0 for s in st2) and outs == blocks
+
+
+def _long_literal_prefix_blocks():
+    """Streams whose first instruction is a long literal run: n >= 239 takes
+    the extension form, n >= 273 its 255-chunk continuation (the first
+    instruction of the block then needs the parser's exact slow path from
+    state ST_F)."""
+    rng = np.random.default_rng(17)
+    out = []
+    for n in (239, 240, 272, 273, 274, 300, 527, 528, 529, 1100, 1300, 3000, 9000):
+        head = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        tail = synth.block(synth.ITB, n, 60000)
+        out.append(head + tail)
+    return out
+
+
+def test_fast_path_takes_every_valid_stream(dev, gu):
+    """The throughput decoder alone (no fallback to the exact decoder) decodes
+    valid streams of every content model and of ITB blocks over the whole C4
+    size range bit-exactly -- so parity is the fast path's, not the safety
+    net's (a parse error the fast path detects would hand the block over)."""
+    blocks = []
+    for kib in (4, 12, 64, 100, 128, 160, 192, 256):
+        blocks += [synth.block(synth.ITB, 1000 * kib + i, kib * 1024) for i in range(3)]
+    for model in range(6):
+        blocks += [synth.block(model, 5000 + model * 10 + i, 65536) for i in range(3)]
+    blocks += _long_literal_prefix_blocks()
+    blocks += [b for b in _adversarial_blocks() if b]
+    comps, st = gu.gpu_compress(torch, blocks, dev)
+    assert all(s == 0 for s in st)
+    outs, st2, fallbacks = gu.gpu_decompress_fast(torch, comps, [len(b) for b in blocks], dev)
+    assert all(s == 0 for s in st2)
+    bad = [i for i, (o, b) in enumerate(zip(outs, blocks)) if o != b]
+    assert not bad, bad[:8]
+    assert fallbacks == 0

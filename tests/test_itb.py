@@ -1,0 +1,106 @@
+"""ITB record codec (mds/itb.c:2904-2980, mdsl/gc.c:755-786) and the MDSL
+append-file loopback (mdsl/storage.c:384-519) on the batch path.
+
+CPU: the append file round trip (host code only).  GPU: the batch wrappers
+against a restatement of the reference's per-ITB logic, with the payload
+compressed by the oracle (the checker): header copied, zlen/len swapped,
+COMPR_LZO set, incompressible ITBs kept as they were; in-place decompression
+restores the record byte for byte.
+"""
+from __future__ import annotations
+
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from pomegranate_amd import itb, synth
+
+
+def _records(n, seed=0, model=synth.ITB):
+    rng = np.random.default_rng(seed)
+    ites = rng.integers(1, 1025, n)
+    ites[:2] = [1, 1024]                     # payload bounds 12,416 and 536,192 bytes
+    return [itb.make_record(seed * 1000 + i, int(k), model) for i, k in enumerate(ites)]
+
+
+def test_append_file_round_trip(tmp_path):
+    """Records cross window boundaries; locations are file offsets; reads are
+    header first, then the rest of h.len."""
+    recs = _records(12, seed=3)
+    path = str(tmp_path / "itb.append")
+    af = itb.AppendFile(path, win=1 << 20)   # ~2-3 records per window
+    locs = [af.append(r[: itb.header_fields(r)[0]]) for r in recs]
+    af.close()
+    want = sum(itb.header_fields(r)[0] for r in recs)
+    assert os.path.getsize(path) == want
+    assert locs[0] == 0 and all(b > a for a, b in zip(locs, locs[1:]))
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        for r, loc in zip(recs, locs):
+            ln = itb.header_fields(r)[0]
+            got = itb.read_record(fd, loc)
+            assert got[:ln] == r[:ln]
+        with pytest.raises(OSError):          # h.len beyond the buffer
+            itb.read_record(fd, locs[1], cap=1000)
+    finally:
+        os.close(fd)
+
+
+def _expected_compress(oracle, rec):
+    """itb_lzo_compress, restated: returns (which, expected oi record bytes)."""
+    ln = itb.header_fields(rec)[0]
+    payload = bytes(rec[itb.ITBH_SIZE:ln])
+    z = oracle.compress(payload)
+    if len(z) >= len(payload):
+        return 0, bytes(rec[:ln])
+    hdr = bytearray(rec[: itb.ITBH_SIZE])
+    struct.pack_into("<II", hdr, itb.LEN_OFF, itb.ITBH_SIZE + len(z), ln)
+    struct.pack_into("<H", hdr, itb.ALGO_OFF, itb.COMPR_LZO)
+    return 1, bytes(hdr) + z
+
+
+@pytest.mark.gpu
+def test_itb_compress_decompress_batch(oracle):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    recs = _records(10, seed=1) + _records(2, seed=2, model=synth.RANDOM)
+    originals = [bytes(r) for r in recs]
+    tmps = [bytearray(itb.ITB_FULL) for _ in recs]
+    which, err = itb.compress_batch(recs, tmps)
+    assert err == [0] * len(recs)
+    outs = []
+    for r, t, w, orig in zip(recs, tmps, which, originals):
+        ew, erec = _expected_compress(oracle, bytearray(orig))
+        assert w == ew
+        o = t if w else r
+        assert bytes(o[: itb.header_fields(o)[0]]) == erec
+        assert bytes(r) == orig                  # the input ITB is untouched
+        outs.append(o)
+    assert which[-2:] == [0, 0]                  # random payloads: impossible to compress
+    # in-place decompression of the compressed ones (mds/itb.c:2949-2980)
+    comp = [bytearray(o) for o, w in zip(outs, which) if w]
+    err, ok = itb.decompress_batch(comp)
+    assert err == [0] * len(comp) and ok == [1] * len(comp)
+    for c, orig in zip(comp, [o for o, w in zip(originals, which) if w]):
+        ln, _, algo = itb.header_fields(c)
+        assert algo == itb.COMPR_NONE and ln == itb.header_fields(bytearray(orig))[0]
+        assert bytes(c[itb.ITBH_SIZE:ln]) == orig[itb.ITBH_SIZE:ln]
+
+
+@pytest.mark.gpu
+def test_itb_decompress_reports_bad_stream():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rec = itb.make_record(7, 3)
+    tmp = bytearray(itb.ITB_FULL)
+    which, err = itb.compress_batch([rec], [tmp])
+    assert which == [1] and err == [0]
+    ln = itb.header_fields(tmp)[0]
+    struct.pack_into("<I", tmp, itb.LEN_OFF, ln - 5)      # truncated payload
+    err, ok = itb.decompress_batch([tmp])
+    assert err[0] != 0 and ok == [0]
+    assert itb.header_fields(tmp)[2] == itb.COMPR_NONE      # flag cleared regardless
