@@ -1,5 +1,5 @@
 // lzo1x_encode_fast.hip -- the throughput LZO1X-1 encoder for MI355X (gfx950)
-// for blocks of up to 64 KiB (ITB-sized).  Output is byte-identical to
+// for blocks of up to 16 MiB (ITB records are 12 KiB - 524 KiB).  Output is byte-identical to
 // lib/minilzo.c:2922-3207 (lzo1x_1_compress) run with a zero-filled wrkmem;
 // the parse is SURVEY.md Appendix A.1.  Larger blocks are left with status
 // LZO_MI355X_ENC_PENDING for lzo1x_encode_kernel (lzo1x_kernels.hip).
@@ -36,17 +36,25 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr uint32_t kSlots = emit::kSlots;
-constexpr uint32_t kMaxN = 65536;               // u16 dictionary positions (p < n - 13)
+// Dictionary entries are u16: v = position - base + 1 (0 = empty).  Before a
+// window could store a value past 65535, the base moves up to a multiple of
+// kRebase at least kM4MaxOffset + 1 below the window, and every entry is
+// re-based: the ones below the new base are cleared -- their distance from
+// every later probe exceeds M4_MAX_OFFSET, so the reference rejects them too
+// (lib/minilzo.c:2878-2883) and the parse is unchanged.
+constexpr uint32_t kRebase = 8192;
+constexpr uint32_t kMaxN = 1u << 24;            // larger blocks: the general encoder
 constexpr uint32_t kTok = 128;                  // token queue entries
 constexpr uint32_t kStage = 2048;               // emitter output ring
 constexpr uint32_t kM2MaxOffset = 0x800;        // lib/minilzo.c M2_MAX_OFFSET
+constexpr uint32_t kNoLane = 0xFFFFFFFFu;
 constexpr uint32_t kM4MaxOffset = 0xBFFF;       // M4_MAX_OFFSET
 #ifndef POM_EMIT_SLEEP
 #define POM_EMIT_SLEEP 8
 #endif
 
 struct __attribute__((aligned(16))) EncLds {
-    uint16_t dict[kSlots];          // last probe position per hash slot (0 = empty)
+    uint16_t dict[kSlots];          // last probe position per hash slot: position - base + 1 (0 = empty)
     uint32_t claim[kSlots / 32];    // per-window slot claims, cleared after each window
     uint4 tok[kTok];                // {literal start, literal count, match length (0: tail), offset}
     uint8_t stage[kStage];          // emitter output ring
@@ -93,12 +101,22 @@ __device__ __forceinline__ void load_at(const uint8_t* in, uint32_t n, uint32_t 
         w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
 }
 
-// Index of the first differing byte of two 16-byte strings (16: none).
-__device__ __forceinline__ uint32_t first_diff16(const uint32_t (&a)[4], const uint32_t (&b)[4])
+#ifndef POM_ENC_CMP
+#define POM_ENC_CMP 4                            // dwords compared in the window round trip
+#endif
+#ifndef POM_ENC_DEFER
+#define POM_ENC_DEFER 0                          // extend a match leaving the window after the cut
+#endif
+constexpr int kCmpW = POM_ENC_CMP;
+constexpr uint32_t kCmpB = 4 * kCmpW;            // match bytes known without an extension
+
+// Index of the first differing byte of two NW-dword strings (4 * NW: none).
+template <int NW>
+__device__ __forceinline__ uint32_t first_diff(const uint32_t (&a)[NW], const uint32_t (&b)[NW])
 {
-    uint32_t m = 16;
+    uint32_t m = 4 * NW;
 #pragma unroll
-    for (int i = 3; i >= 0; i--) {
+    for (int i = NW - 1; i >= 0; i--) {
         const uint32_t x = a[i] ^ b[i];
         m = x ? 4u * i + ((uint32_t)__builtin_ctz(x) >> 3) : m;
     }
@@ -133,15 +151,35 @@ __device__ uint32_t extend_match(const uint8_t* in, uint32_t n, uint32_t mc, uin
 // ---------------------------------------------------------------------------
 // Parse wave
 // ---------------------------------------------------------------------------
-__device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
+// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums and counts of
+// the parse wave go to stamps[b * kEncStampSlots + i]; no output depends on them.
+enum { EP_SETUP, EP_PROBE, EP_CAND, EP_PATH, EP_CLAIM, EP_TOK, EP_DICT, EP_PUSHWAIT,
+       EC_WINDOWS, EC_EXTEND, EC_TOKENS, EP_N };
+constexpr int kEncStampSlots = 16;
+
+template <bool STAMPS>
+__device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l, uint64_t* acc)
 {
+    uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+#define ESTAMP(ph)                                                  \
+    do {                                                            \
+        if (STAMPS) {                                               \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+            acc[ph] += now_ - tmark;                                \
+            tmark = now_;                                           \
+        }                                                           \
+    } while (0)
     uint32_t tp = 0;                                // tokens produced
     uint32_t cons_seen = 0;
     auto push = [&](uint32_t from, uint32_t nlit, uint32_t mlen, uint32_t off) {
+        if (STAMPS)
+            acc[EC_TOKENS] += 1;
+        ESTAMP(EP_TOK);
         while (tp - cons_seen >= kTok) {             // the emit wave always drains
             __builtin_amdgcn_s_sleep(2);
             cons_seen = lds_load(&S.cons);
         }
+        ESTAMP(EP_PUSHWAIT);
         if (l == 0)
             S.tok[tp % kTok] = make_uint4(from, nlit, mlen, off);
         tp++;
@@ -157,36 +195,60 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
         wave_order();
         const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
         uint32_t ip = 4;
+        uint32_t base = 0;                          // dictionary position base
+        ESTAMP(EP_SETUP);
         for (;;) {
+            if (STAMPS)
+                acc[EC_WINDOWS] += 1;
+            if (ip + kWave - base >= 0xFFFFu) {     // this window's positions would not fit
+                const uint32_t nb = (ip - (kM4MaxOffset + 1)) / kRebase * kRebase;
+                const uint32_t delta = nb - base;
+                for (uint32_t s2 = l; s2 < kSlots / 2; s2 += kWave) {
+                    const uint32_t pr = ((uint32_t*)S.dict)[s2];
+                    const uint32_t lo = pr & 0xFFFFu, hi = pr >> 16;
+                    const uint32_t nlo = lo > delta ? lo - delta : 0u;
+                    const uint32_t nhi = hi > delta ? hi - delta : 0u;
+                    ((uint32_t*)S.dict)[s2] = nlo | (nhi << 16);
+                }
+                wave_order();
+                base = nb;
+            }
             const uint32_t p = ip + l;
             const bool active = l == 0 || p < ip_end;   // the first probe always runs
-            uint32_t pw[4] = {0, 0, 0, 0};
+            uint32_t pw[kCmpW] = {};
             uint32_t h1 = 0, h2 = 0, w1 = 0, w2 = 0;
             if (active) {
-                load_at<4>(in, n, p, pw);
+                load_at<kCmpW>(in, n, p, pw);
                 const uint32_t b0 = pw[0] & 0xFF, b1 = (pw[0] >> 8) & 0xFF;
                 const uint32_t b2 = (pw[0] >> 16) & 0xFF, b3 = pw[0] >> 24;
                 h1 = emit::slot_primary(b0, b1, b2, b3);
                 h2 = emit::slot_secondary(h1);
-                w1 = S.dict[h1];
-                w2 = S.dict[h2];
+                const uint32_t e1 = S.dict[h1], e2 = S.dict[h2];
+                w1 = e1 ? base + e1 - 1 : 0u;           // (positions >= 4: 0 stays "empty")
+                w2 = e2 ? base + e2 - 1 : 0u;
             }
             const uint64_t am = wave_ballot(active);
             const uint32_t nact = (uint32_t)__builtin_popcountll(am);
+            if (STAMPS)
+                __builtin_amdgcn_s_waitcnt(0);       // (attribute the probe loads here)
+            ESTAMP(EP_PROBE);
 
             // Probe decision of every active lane with the pre-window
             // dictionary, lib/minilzo.c:2940-2971 (exact up to the cut below).
             const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
             const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
-            uint32_t c1w[4] = {0, 0, 0, 0}, c2w[4] = {0, 0, 0, 0};
+            uint32_t c1w[kCmpW] = {}, c2w[kCmpW] = {};
             if (v1)
-                load_at<4>(in, n, w1, c1w);
+                load_at<kCmpW>(in, n, w1, c1w);
             if (v2)
-                load_at<4>(in, n, w2, c2w);
+                load_at<kCmpW>(in, n, w2, c2w);
             const uint32_t b3 = pw[0] >> 24;
             bool tm = false;
             uint32_t slot = h1, cand = w1;
-            uint32_t cw[4] = {c1w[0], c1w[1], c1w[2], c1w[3]};
+            uint32_t cw[kCmpW];
+#pragma unroll
+            for (int i = 0; i < kCmpW; i++)
+                cw[i] = c1w[i];
             if (v1) {
                 if (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3) {
                     tm = true;
@@ -196,14 +258,14 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
                         tm = true;
                         cand = w2;
 #pragma unroll
-                        for (int i = 0; i < 4; i++)
+                        for (int i = 0; i < kCmpW; i++)
                             cw[i] = c2w[i];
                     }
                 }
             }
-            // try_match (:2962-2971), then the match length as far as 16 bytes
+            // try_match (:2962-2971), then the match length as far as kCmpB bytes
             const bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
-            uint32_t mlen = first_diff16(cw, pw);
+            uint32_t mlen = first_diff<kCmpW>(cw, pw);
             mlen = mlen < n - p ? mlen : n - p;
 
             // ---- the greedy path through the window, speculatively ----------
@@ -211,8 +273,10 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
             // lane is a literal.  Lanes inside matches neither probe nor
             // update the dictionary (:3051-3150).
             const uint64_t okm = wave_ballot(ok);
+            ESTAMP(EP_CAND);
             uint64_t path = 0, mstart = 0;
             uint32_t end = 0;                        // lane where the path leaves the window
+            uint32_t deferred = kNoLane;             // a match left unextended: it leaves the window anyway
             while (end < nact) {
                 const uint64_t rest = okm & (~0ull << end);
                 const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
@@ -226,13 +290,21 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
                 path |= 1ull << q;
                 mstart |= 1ull << q;
                 uint32_t len = lane_read(mlen, q);
-                if (len == 16 && n - (ip + q) > 16) {
-                    len = extend_match(in, n, lane_read(cand, q), ip + q, 16, l);
+                if (len == kCmpB && n - (ip + q) > kCmpB) {
+                    if (POM_ENC_DEFER && q + kCmpB >= nact) {   // its length only matters if kept
+                        deferred = q;
+                        end = q + kCmpB;
+                        break;
+                    }
+                    if (STAMPS)
+                        acc[EC_EXTEND] += 1;
+                    len = extend_match(in, n, lane_read(cand, q), ip + q, kCmpB, l);
                     mlen = l == q ? len : mlen;
                 }
                 end = q + len;
             }
 
+            ESTAMP(EP_PATH);
             // ---- exactness: claims among the path lanes only ------------------
             // Path lane l reads its two slots and writes one of them.  Of two
             // path lanes sharing a slot at least one sees the other's bit
@@ -266,8 +338,17 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
 #endif
             if (cut < end)                           // the window ends at a path lane
                 end = cut;
+            if (deferred != kNoLane && deferred < end) {   // the unextended match is kept: its length
+                if (STAMPS)
+                    acc[EC_EXTEND] += 1;
+                const uint32_t len = extend_match(in, n, lane_read(cand, deferred), ip + deferred,
+                                                  kCmpB, l);
+                mlen = l == deferred ? len : mlen;
+                end = deferred + len;
+            }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
 
+            ESTAMP(EP_CLAIM);
             // ---- tokens for the matches before the cut ------------------------
             bool done = false;
             for (uint64_t mm = mstart & keep; mm; mm &= mm - 1) {
@@ -282,9 +363,11 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
                 }
             }
             // UPDATE_I of every path lane before the cut; their slots are distinct
+            ESTAMP(EP_TOK);
             if ((path & keep) >> l & 1ull)
-                S.dict[slot] = (uint16_t)p;
+                S.dict[slot] = (uint16_t)(p - base + 1);
             wave_order();
+            ESTAMP(EP_DICT);
             if (done)
                 break;
             ip += end;
@@ -293,6 +376,7 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l)
         }
     }
     push(ii, n - ii, 0, 0);                          // tail + EOF
+#undef ESTAMP
 }
 
 // ---------------------------------------------------------------------------
@@ -311,6 +395,8 @@ __device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out
     e.sflush = kStage / 2;
     e.op = e.flushed = 0;
     uint32_t ct = 0;                                 // tokens consumed
+    uint32_t pos = 0;                                // input covered by the tokens so far
+    bool poisoned = false;                           // a token the parse cannot have meant
     for (;;) {
         const uint32_t prod = lds_load(&S.prod);
         if (ct == prod) {
@@ -320,37 +406,51 @@ __device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out
         while (ct < prod) {
             const uint4 t = S.tok[ct % kTok];
             ct++;
+            // Every token must continue where the last one ended and stay in
+            // the block, a match must look back into it: otherwise nothing is
+            // emitted (no read past the input), the queue is still drained so
+            // the parse wave never blocks, and the block reports LZO_E_ERROR.
+            poisoned = poisoned || t.x != pos || t.y > n - pos ||
+                       (t.z != 0 && (t.z > n - pos - t.y || t.w == 0 || t.w > pos + t.y ||
+                                     t.w > kM4MaxOffset));
             if (t.z == 0) {                          // tail literals + EOF: the block is done
-                emit::tail_and_eof(e, t.x);
+                if (!poisoned && t.y == n - pos)
+                    emit::tail_and_eof(e, t.x);
                 if (lane_id() == 0) {
                     out_len[b] = e.op;
-                    status[b] = e.op <= e.cap ? 0 : -5;    // LZO_E_OK / LZO_E_OUTPUT_OVERRUN
+                    status[b] = poisoned || t.y != n - pos ? -1          // LZO_E_ERROR
+                              : e.op <= e.cap ? 0 : -5;  // LZO_E_OK / LZO_E_OUTPUT_OVERRUN
                 }
                 return;
             }
-            if (t.y) {
-                emit::lit_header(e, t.y);
-                emit::lits(e, t.x, t.y);
+            if (!poisoned) {
+                if (t.y) {
+                    emit::lit_header(e, t.y);
+                    emit::lits(e, t.x, t.y);
+                }
+                emit::match(e, t.z, t.w);
+                emit::maybe_flush(e);
+                pos += t.y + t.z;
             }
-            emit::match(e, t.z, t.w);
-            emit::maybe_flush(e);
             lds_store(&S.cons, ct);
         }
     }
 }
 
+template <bool STAMPS>
 __global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks)
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
+    uint64_t* __restrict__ stamps)
 {
     __shared__ EncLds S;
     const uint32_t b = blockIdx.x;
     if (b >= nblocks)
         return;
     const uint32_t n = src_len[b];
-    if (n > kMaxN) {                                 // positions must fit the u16 dictionary
+    if (n > kMaxN) {                                 // (u32 positions, 16-bit token lengths kept small)
         if (threadIdx.x == 0)
             status[b] = LZO_MI355X_ENC_PENDING;
         return;
@@ -363,9 +463,13 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
     }
     __syncthreads();
     const uint8_t* in = src + src_off[b];
-    if (wave == 0)
-        parse_wave(S, in, n, l);
-    else
+    if (wave == 0) {
+        uint64_t acc[EP_N] = {};
+        parse_wave<STAMPS>(S, in, n, l, acc);
+        if (STAMPS && l == 0)
+            for (int i = 0; i < EP_N; i++)
+                stamps[(size_t)b * kEncStampSlots + i] = acc[i];
+    } else
         emit_wave(S, in, n, dst + dst_off[b], dst_cap[b], out_len, status, b);
 }
 
@@ -379,7 +483,24 @@ extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_encode_fast_kernel, dim3(nblocks), dim3(2 * kWave), 0, stream, src,
-                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
+    hipLaunchKernelGGL(lzo1x_encode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
+                       nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Diagnostic: the same encoder with parse-wave phase stamps (16 x u64 per block).
+extern "C" int lzo_mi355x_debug_compress_fast_stamps(const uint8_t* src, const uint64_t* src_off,
+                                                     const uint32_t* src_len, uint8_t* dst,
+                                                     const uint64_t* dst_off,
+                                                     const uint32_t* dst_cap, uint32_t* out_len,
+                                                     int32_t* status, uint32_t nblocks,
+                                                     uint64_t* stamps, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_encode_fast_kernel<true>, dim3(nblocks), dim3(2 * kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
+                       stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -146,7 +146,7 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                             uint32_t *out_len, int32_t *status, uint32_t nblocks,
                             void *stream)
 {
-    /* blocks up to 64 KiB: the throughput encoder; larger ones are left
+    /* blocks up to 16 MiB: the throughput encoder; larger ones are left
      * pending for the general encoder, whose other workgroups exit at once */
     hipStream_t s = (hipStream_t)stream;
     if (nblocks == 0)
@@ -208,6 +208,66 @@ int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,
 /* ------------------------------------------------------------------------ */
 /* Host-resident batches: pack -> H2D -> kernels -> D2H -> unpack           */
 /* ------------------------------------------------------------------------ */
+/* Pack/unpack copies between caller buffers and the pinned staging: split
+ * over up to kCopyThreads threads by bytes once a batch is large enough for
+ * one memcpy stream to be the bottleneck (the host side of config C5). */
+struct copy_job {
+    uint8_t *dst;
+    const uint8_t *src;
+    size_t len;
+};
+
+struct copy_range {
+    const struct copy_job *jobs;
+    size_t lo, hi;
+};
+
+enum { kCopyThreads = 8 };
+static const size_t kCopyParallelBytes = 8u << 20;
+
+static void *copy_worker(void *arg)
+{
+    const struct copy_range *r = arg;
+    for (size_t i = r->lo; i < r->hi; i++)
+        if (r->jobs[i].len)
+            memcpy(r->jobs[i].dst, r->jobs[i].src, r->jobs[i].len);
+    return NULL;
+}
+
+static void copy_jobs(const struct copy_job *jobs, size_t n)
+{
+    size_t total = 0;
+    for (size_t i = 0; i < n; i++)
+        total += jobs[i].len;
+    struct copy_range r[kCopyThreads];
+    pthread_t th[kCopyThreads];
+    int nt = total >= kCopyParallelBytes && n > 1 ? kCopyThreads : 1;
+    /* contiguous job ranges of about total / nt bytes each */
+    size_t i = 0, acc = 0;
+    int k = 0;
+    for (; k < nt && i < n; k++) {
+        r[k].jobs = jobs;
+        r[k].lo = i;
+        const size_t goal = total / (size_t)nt * (size_t)(k + 1);
+        while (i < n && (acc < goal || k == nt - 1)) {
+            acc += jobs[i].len;
+            i++;
+        }
+        r[k].hi = i;
+    }
+    int started = 0;
+    for (int j = 1; j < k; j++)
+        if (pthread_create(&th[j], NULL, copy_worker, &r[j]) == 0)
+            started |= 1 << j;
+        else
+            copy_worker(&r[j]);
+    if (k > 0)
+        copy_worker(&r[0]);
+    for (int j = 1; j < k; j++)
+        if (started & (1 << j))
+            pthread_join(th[j], NULL);
+}
+
 /* Staging layout (identical on host and device, so one copy each way):
  *   [src_off u64][dst_off u64][src_len u32][dst_cap u32][out_len u32][status i32]
  *   [src bytes, 16-B aligned per block][dst bytes, 16-B aligned per block] */
@@ -253,15 +313,25 @@ static void layout_fill(const struct layout *L, uint8_t *h, const uint8_t *const
     uint32_t *sl = (uint32_t *)(h + L->o_srclen);
     uint32_t *dc = (uint32_t *)(h + L->o_dstcap);
     size_t s = 0, d = 0;
+    struct copy_job *jobs = malloc(L->nb * sizeof(*jobs));
     for (size_t b = 0; b < L->nb; b++) {
         so[b] = s;
         dof[b] = d;
         sl[b] = (uint32_t)src_len[b];
         dc[b] = (uint32_t)dst_cap[b];
-        if (src_len[b])
+        if (jobs) {
+            jobs[b].dst = h + L->o_src + s;
+            jobs[b].src = src[b];
+            jobs[b].len = src_len[b];
+        } else if (src_len[b]) {
             memcpy(h + L->o_src + s, src[b], src_len[b]);
+        }
         s += ALIGN_UP(src_len[b], 16);
         d += ALIGN_UP(dst_cap[b], 16);
+    }
+    if (jobs) {
+        copy_jobs(jobs, L->nb);
+        free(jobs);
     }
 }
 
@@ -332,12 +402,22 @@ static int batch_common(enum op_kind kind, const uint8_t *const *src, const size
             const uint32_t *ol = (const uint32_t *)(t->hmem + L.o_outlen);
             const int32_t *st = (const int32_t *)(t->hmem + L.o_status);
             const uint64_t *dof = (const uint64_t *)(t->hmem + L.o_dstoff);
+            struct copy_job *jobs = malloc(nblocks * sizeof(*jobs));
             for (size_t b = 0; b < nblocks; b++) {
                 size_t n = ol[b] < cap[b] ? ol[b] : cap[b];
-                if (n)
+                if (jobs) {
+                    jobs[b].dst = dst[b];
+                    jobs[b].src = t->hmem + L.o_dst + dof[b];
+                    jobs[b].len = n;
+                } else if (n) {
                     memcpy(dst[b], t->hmem + L.o_dst + dof[b], n);
+                }
                 dst_len[b] = ol[b];
                 status[b] = st[b];
+            }
+            if (jobs) {
+                copy_jobs(jobs, nblocks);
+                free(jobs);
             }
             rc = LZO_E_OK;
         }

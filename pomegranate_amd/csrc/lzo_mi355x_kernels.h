@@ -14,7 +14,7 @@ extern "C" {
 /* status of a block lzo1x_encode_fast_kernel left to the general encoder */
 #define LZO_MI355X_ENC_PENDING 0x7FFF0002
 
-/* Throughput encoder (lzo1x_encode_fast.hip), blocks of up to 64 KiB; larger
+/* Throughput encoder (lzo1x_encode_fast.hip), blocks of up to 16 MiB; larger
  * blocks get status LZO_MI355X_ENC_PENDING. */
 int lzo_mi355x_launch_compress_fast(const uint8_t *src, const uint64_t *src_off,
                                     const uint32_t *src_len, uint8_t *dst,
