@@ -211,3 +211,41 @@ def test_fast_path_takes_every_valid_stream(dev, gu):
     bad = [i for i, (o, b) in enumerate(zip(outs, blocks)) if o != b]
     assert not bad, bad[:8]
     assert fallbacks == 0
+
+
+def _mutated_streams(oracle, count=192, seed=23):
+    """Valid ITB streams with the damage real storage or wire errors do: a few
+    flipped bytes, a truncation, trailing garbage, a zeroed run."""
+    rng = np.random.default_rng(seed)
+    base = [oracle.compress(synth.block(synth.ITB, 900 + i, 65536)) for i in range(8)]
+    out = []
+    for i in range(count):
+        z = bytearray(base[i % len(base)])
+        kind = i % 4
+        if kind == 0:
+            for _ in range(int(rng.integers(1, 4))):
+                z[int(rng.integers(0, len(z)))] ^= int(rng.integers(1, 256))
+        elif kind == 1:
+            z = z[: int(rng.integers(1, len(z)))]
+        elif kind == 2:
+            z += rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8).tobytes()
+        else:
+            a, k = int(rng.integers(0, len(z) - 16)), int(rng.integers(1, 16))
+            z[a: a + k] = bytes(k)
+        out.append(bytes(z))
+    return out
+
+
+def test_decompress_mutated_streams_vs_oracle(dev, gu, oracle):
+    """Damaged streams through the whole GPU path (fast decoder, refusal,
+    exact decoder): LZO_E_* code, produced length and produced bytes equal
+    lzo1x_decompress_safe's (the oracle), at capacity n and n/2."""
+    streams = _mutated_streams(oracle)
+    caps = [65536 if i % 3 else 32768 for i in range(len(streams))]
+    outs, st, _ = gu.gpu_decompress(torch, streams, caps, dev)
+    bad = []
+    for i, (z, c) in enumerate(zip(streams, caps)):
+        rc, want = oracle.decompress_safe(z, c)
+        if st[i] != rc or outs[i] != want:
+            bad.append((i, st[i], rc, len(outs[i]), len(want)))
+    assert not bad, bad[:6]
