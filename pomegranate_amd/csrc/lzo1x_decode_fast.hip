@@ -338,17 +338,14 @@ __device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint
                                             bool* slow = nullptr)
 {
     const uint32_t rel = pos - k.P;
-    const bool inwin = rel + 12 <= kStageBytes && pos < k.z;
-    // The 8 bytes at pos (read unconditionally from a clamped window offset;
-    // ignored when !inwin).
+    const bool inwin = rel + 8 <= kStageBytes && pos < k.z;
+    // Every field of a non-extended instruction lies in its first 4 bytes
+    // (t, then at most 3 more; bytes past z read 0 from the stage): two LDS
+    // dwords, one alignbyte, then bit-field extracts -- no 64-bit shifts.
+    // (The dwords are read from a clamped offset; ignored when !inwin.)
     const uint32_t wi = inwin ? rel >> 2 : 0u;
-    const uint32_t w0 = s.stage[wi], w1 = s.stage[wi + 1], w2 = s.stage[wi + 2];
-    const uint32_t sh = 8u * (rel & 3u);
-    const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
-    const uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
-    const uint64_t b8 = ((uint64_t)hi << 32) | lo;                 // bytes pos..pos+7
-#define BYTE(i) ((uint32_t)(b8 >> (8u * (i))) & 0xFFu)
-    const uint32_t t = lo & 0xFFu, b1 = BYTE(1);
+    const uint32_t lo = __builtin_amdgcn_alignbyte(s.stage[wi + 1], s.stage[wi], rel & 3u);
+    const uint32_t t = lo & 0xFFu, b1 = __builtin_amdgcn_ubfe(lo, 8, 8);
     const bool flit = st == ST_F && t > 17;                        // :3357-3365
     const uint32_t se = st == ST_F ? ST_A : st;
     const bool lit = !flit && se == ST_A && t < 16;                // :3367-3414
@@ -359,11 +356,10 @@ __device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint
     const bool ext = (lit && t == 0) || (m3 && (t & 31) == 0) || (m4 && (t & 7) == 0);
     const bool needs_slow = !inwin || (ext && b1 == 0);            // 255-chunk extension
     const uint32_t e = ext ? 1u : 0u;
-    const uint32_t o16 = BYTE(1 + e) | (BYTE(2 + e) << 8);
+    const uint32_t o16 = __builtin_amdgcn_ubfe(lo, 8u + 8u * e, 16);   // bytes 1+e, 2+e
     const uint32_t dd4 = ((t & 8u) << 11) + (o16 >> 2);
     const uint32_t used = (m1 || m2) ? 2u : 3u + e;                // match instruction bytes
-    const uint32_t tl = BYTE(used - 2) & 3u;                       // match_done, :3650
-#undef BYTE
+    const uint32_t tl = __builtin_amdgcn_ubfe(lo, 8u * (used - 2u), 2);   // match_done, :3650
     const uint32_t nlit = flit ? t - 17 : (ext ? 15u + b1 : t) + 3u;
     const uint32_t L = m1 ? (se == ST_B ? 3u : 2u)
                      : m2 ? (t >> 5) + 1u
@@ -800,6 +796,13 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
         __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
         lds_store(&S.pinfo[q & (kSlots - 1)],
                   total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u) | (reason << 20));
+#ifdef POM_EXPERIMENT_RECORD
+        // (timing experiment only: every piece keeps its slot; the piece
+        // infos go to the last slot for an executor-only replay)
+        if (l == 0)
+            ((uint32_t*)(gops + (kSlots - 1) * kOpMax))[q] =
+                total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u);
+#endif
         lds_store(&S.parsed, q + 1);
         STAMP(PH_WRITE);
         if (err || eof)
@@ -1017,6 +1020,31 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
     uint32_t reason = refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
     if (wave == 1) {
+#ifdef POM_EXPERIMENT_REPLAY
+        // (timing experiment only: publish the recorded pieces at once, then
+        // only the writer duty runs)
+        if (!refuse) {
+            const uint32_t* rec = (const uint32_t*)(gops + (kSlots - 1) * kOpMax);
+            uint32_t nq = 0;
+            for (; nq < kSlots - 1; nq++) {
+                const uint32_t info = rec[nq];
+                S.pinfo[nq] = info;
+                if (info & (kInfoEof | kInfoErr))
+                    break;
+            }
+            wave_order();
+            lds_store(&S.parsed, nq + 1);
+            WState w;
+            w.issued = 0;
+            w.landed = 0;
+            for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+                if (writer_duty(S, k.out, l, w) != 0)
+                    break;
+                __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
+            }
+        }
+        return;
+#endif
         if (!refuse)
             parser_wave<STAMPS>(S, k, gops, l, acc);
         if (STAMPS && l == 0)
