@@ -52,6 +52,9 @@ constexpr uint32_t kM4MaxOffset = 0xBFFF;       // M4_MAX_OFFSET
 #ifndef POM_EMIT_SLEEP
 #define POM_EMIT_SLEEP 8
 #endif
+#ifndef POM_ENC_AHEAD
+#define POM_ENC_AHEAD 2048                      // bytes the emit wave pulls into L2 ahead of the parse
+#endif
 
 struct __attribute__((aligned(16))) EncLds {
     uint16_t dict[kSlots];          // last probe position per hash slot: position - base + 1 (0 = empty)
@@ -60,6 +63,8 @@ struct __attribute__((aligned(16))) EncLds {
     uint8_t stage[kStage];          // emitter output ring
     uint32_t prod;                  // tokens published by the parse wave
     uint32_t cons;                  // tokens consumed by the emit wave
+    uint32_t ip;                    // the parse wave's window start (a prefetch hint)
+    uint32_t sink;                  // prefetched words end here
 };
 // four blocks (eight waves) per CU
 static_assert(sizeof(EncLds) * 4 <= 160 * 1024, "LDS budget");
@@ -213,6 +218,8 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 wave_order();
                 base = nb;
             }
+            if (POM_ENC_AHEAD)
+                S.ip = ip;
             const uint32_t p = ip + l;
             const bool active = l == 0 || p < ip_end;   // the first probe always runs
             uint32_t pw[kCmpW] = {};
@@ -397,7 +404,31 @@ __device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out
     uint32_t ct = 0;                                 // tokens consumed
     uint32_t pos = 0;                                // input covered by the tokens so far
     bool poisoned = false;                           // a token the parse cannot have meant
+    // Lines ahead of the parse wave go to L2 from this wave, so the parse
+    // wave's probe, candidate and extension loads hit there: one dword per
+    // 128-B line, 8 KiB per load instruction; waiting on them stalls only
+    // this wave.
+    const uintptr_t lines = (uintptr_t)in & ~(uintptr_t)127;
+    const uintptr_t last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
+    uint32_t pf = 0;                                 // bytes from `lines` already touched
+    auto prefetch = [&]() {
+        if (!POM_ENC_AHEAD)
+            return;
+        const uint32_t ahead = *(volatile uint32_t*)&S.ip + POM_ENC_AHEAD;
+        const uint32_t want = ahead < n + 127 ? ahead : n + 127;
+        if (pf >= want)
+            return;
+        uint32_t x = 0;
+        for (; pf < want; pf += 128 * kWave) {
+            const uintptr_t a = lines + pf + 128 * lane_id();
+            if (a <= last)
+                x ^= *(gdword*)a;
+        }
+        if (x == 0x9E3779B9u)                        // (keeps the loads; never matters)
+            S.sink = x;
+    };
     for (;;) {
+        prefetch();
         const uint32_t prod = lds_load(&S.prod);
         if (ct == prod) {
             __builtin_amdgcn_s_sleep(POM_EMIT_SLEEP);
@@ -460,6 +491,7 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
     if (threadIdx.x == 0) {
         S.prod = 0;
         S.cons = 0;
+        S.ip = 0;
     }
     __syncthreads();
     const uint8_t* in = src + src_off[b];
