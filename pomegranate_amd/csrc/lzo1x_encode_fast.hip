@@ -85,25 +85,41 @@ __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
 
 typedef __attribute__((address_space(1))) const uint32_t gdword;
 
-// NW little-endian dwords of the block starting at byte pos (any alignment).
-// Aligned dwords lying wholly past the block's last byte are not read (0):
-// callers cap every comparison at the block end.  Address-space-1 loads keep
-// these global_load (vmcnt), not flat_load.
-template <int NW>
-__device__ __forceinline__ void load_at(const uint8_t* in, uint32_t n, uint32_t pos, uint32_t (&w)[NW])
+// The block as a raw buffer: the aligned dwords from the one holding byte 0
+// through the one holding byte n-1.  Reads past it return 0 in hardware (the
+// range check), so every probe, candidate and extension load is unconditional
+// -- no exec branches, and the loads of one round trip share one wait.
+struct BlockSrc {
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t sh0;                                   // in & 3
+};
+
+__device__ __forceinline__ BlockSrc block_src(const uint8_t* in, uint32_t n)
 {
-    const uintptr_t a = (uintptr_t)in + pos;
-    const uintptr_t a0 = a & ~(uintptr_t)3;
-    const uintptr_t last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
-    gdword* q = (gdword*)a0;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)in);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)in >> 32));
+    const uint32_t nn = __builtin_amdgcn_readfirstlane(n);
+    const uintptr_t base = (((uintptr_t)hi << 32) | lo) & ~(uintptr_t)3;
+    const uint32_t sh0 = lo & 3u;
+    const uint32_t bytes = nn ? ((sh0 + nn - 1) & ~3u) + 4u : 0u;
+    return {__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000), sh0};
+}
+
+// NW little-endian dwords of the block starting at byte pos (any alignment).
+// Aligned dwords lying wholly past the block's last byte read as 0: callers
+// cap every comparison at the block end.
+template <int NW>
+__device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_t (&w)[NW])
+{
+    const uint32_t a = pos + B.sh0;
+    const uint32_t a0 = a & ~3u;
     uint32_t r[NW + 1];
 #pragma unroll
     for (int i = 0; i <= NW; i++)
-        r[i] = a0 + 4 * i <= last ? q[i] : 0u;
-    const uint32_t sh = (uint32_t)(a & 3);
+        r[i] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, a0 + 4 * i, 0, 0);
 #pragma unroll
     for (int i = 0; i < NW; i++)
-        w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);
+        w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], a & 3u);
 }
 
 #ifndef POM_ENC_CMP
@@ -130,21 +146,17 @@ __device__ __forceinline__ uint32_t first_diff(const uint32_t (&a)[NW], const ui
 
 // Match length from index k0 on (the first k0 bytes match), wave-parallel,
 // 256 bytes per round trip, capped at the block end (lib/minilzo.c:3090-3102).
-__device__ uint32_t extend_match(const uint8_t* in, uint32_t n, uint32_t mc, uint32_t mp,
+__device__ uint32_t extend_match(const BlockSrc& B, uint32_t n, uint32_t mc, uint32_t mp,
                                  uint32_t k0, uint32_t l)
 {
     const uint32_t lim = n - mp;
     for (uint32_t k = k0;; k += 4 * kWave) {
         const uint32_t idx = k + 4 * l;
-        uint32_t e = 0xFFFFFFFFu;
-        if (idx < lim) {
-            uint32_t a[1], b[1];
-            load_at<1>(in, n, mc + idx, a);
-            load_at<1>(in, n, mp + idx, b);
-            const uint32_t x = a[0] ^ b[0];
-            if (x)
-                e = idx + ((uint32_t)__builtin_ctz(x) >> 3);
-        }
+        uint32_t a[1], b[1];
+        load_at<1>(B, mc + idx, a);
+        load_at<1>(B, mp + idx, b);
+        const uint32_t x = a[0] ^ b[0];
+        uint32_t e = idx < lim && x ? idx + ((uint32_t)__builtin_ctz(x) >> 3) : 0xFFFFFFFFu;
         if (idx + 4 > lim)
             e = e < lim ? e : lim;
         const uint64_t mis = wave_ballot(e != 0xFFFFFFFFu);
@@ -191,6 +203,7 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
         lds_store(&S.prod, tp);
     };
 
+    const BlockSrc B = block_src(in, n);
     uint32_t ii = 0;                                // first byte not yet emitted
     if (n > 13) {                                   // lib/minilzo.c:3167-3173
         for (uint32_t s = l; s < kSlots / 2; s += kWave)
@@ -222,10 +235,10 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 S.ip = ip;
             const uint32_t p = ip + l;
             const bool active = l == 0 || p < ip_end;   // the first probe always runs
-            uint32_t pw[kCmpW] = {};
+            uint32_t pw[kCmpW];
+            load_at<kCmpW>(B, p, pw);
             uint32_t h1 = 0, h2 = 0, w1 = 0, w2 = 0;
             if (active) {
-                load_at<kCmpW>(in, n, p, pw);
                 const uint32_t b0 = pw[0] & 0xFF, b1 = (pw[0] >> 8) & 0xFF;
                 const uint32_t b2 = (pw[0] >> 16) & 0xFF, b3 = pw[0] >> 24;
                 h1 = emit::slot_primary(b0, b1, b2, b3);
@@ -244,11 +257,9 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             // dictionary, lib/minilzo.c:2940-2971 (exact up to the cut below).
             const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
             const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
-            uint32_t c1w[kCmpW] = {}, c2w[kCmpW] = {};
-            if (v1)
-                load_at<kCmpW>(in, n, w1, c1w);
-            if (v2)
-                load_at<kCmpW>(in, n, w2, c2w);
+            uint32_t c1w[kCmpW], c2w[kCmpW];        // (read unconditionally; used only if valid)
+            load_at<kCmpW>(B, w1, c1w);
+            load_at<kCmpW>(B, w2, c2w);
             const uint32_t b3 = pw[0] >> 24;
             bool tm = false;
             uint32_t slot = h1, cand = w1;
@@ -305,7 +316,7 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                     }
                     if (STAMPS)
                         acc[EC_EXTEND] += 1;
-                    len = extend_match(in, n, lane_read(cand, q), ip + q, kCmpB, l);
+                    len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
                     mlen = l == q ? len : mlen;
                 }
                 end = q + len;
@@ -348,7 +359,7 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             if (deferred != kNoLane && deferred < end) {   // the unextended match is kept: its length
                 if (STAMPS)
                     acc[EC_EXTEND] += 1;
-                const uint32_t len = extend_match(in, n, lane_read(cand, deferred), ip + deferred,
+                const uint32_t len = extend_match(B, n, lane_read(cand, deferred), ip + deferred,
                                                   kCmpB, l);
                 mlen = l == deferred ? len : mlen;
                 end = deferred + len;
