@@ -123,7 +123,7 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 }
 
 #ifndef POM_ENC_CMP
-#define POM_ENC_CMP 4                            // dwords compared in the window round trip
+#define POM_ENC_CMP 8                            // dwords compared in the window round trip
 #endif
 #ifndef POM_ENC_DEFER
 #define POM_ENC_DEFER 0                          // extend a match leaving the window after the cut
@@ -214,6 +214,11 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
         const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
         uint32_t ip = 4;
         uint32_t base = 0;                          // dictionary position base
+        // Probe words of the window (position ip + l): the next window's are
+        // read as soon as its start is known, ahead of the token and
+        // dictionary writes.
+        uint32_t pw[kCmpW];
+        load_at<kCmpW>(B, ip + l, pw);
         ESTAMP(EP_SETUP);
         for (;;) {
             if (STAMPS)
@@ -235,8 +240,6 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 S.ip = ip;
             const uint32_t p = ip + l;
             const bool active = l == 0 || p < ip_end;   // the first probe always runs
-            uint32_t pw[kCmpW];
-            load_at<kCmpW>(B, p, pw);
             uint32_t h1 = 0, h2 = 0, w1 = 0, w2 = 0;
             if (active) {
                 const uint32_t b0 = pw[0] & 0xFF, b1 = (pw[0] >> 8) & 0xFF;
@@ -366,19 +369,44 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
 
+            uint32_t npw[kCmpW];
+            load_at<kCmpW>(B, ip + end + l, npw);
+
             ESTAMP(EP_CLAIM);
             // ---- tokens for the matches before the cut ------------------------
-            bool done = false;
-            for (uint64_t mm = mstart & keep; mm; mm &= mm - 1) {
-                const uint32_t q = (uint32_t)__builtin_ctzll(mm);
-                const uint32_t mp = ip + q;
-                const uint32_t len = lane_read(mlen, q);
-                push(ii, mp - ii, len, mp - lane_read(cand, q));
-                ii = mp + len;
-                if (ii >= ip_end) {                  // :3151-3152
-                    done = true;
-                    break;
+            // Each match lane writes its own token: its literal run starts
+            // after the highest lane below it that is not a literal path lane
+            // (the last byte of the previous match), or at ii.  The parse
+            // stops after the first match reaching ip_end (:3151-3152).
+            uint64_t km = mstart & keep;
+            const bool ism = (km >> l) & 1ull;
+            const uint64_t dm = wave_ballot(ism && p + mlen >= ip_end);
+            const bool done = dm != 0;
+            if (done) {
+                const uint32_t d = (uint32_t)__builtin_ctzll(dm);
+                km &= d >= 63 ? ~0ull : ((2ull << d) - 1);
+            }
+            if (km) {
+                const uint32_t cnt = (uint32_t)__builtin_popcountll(km);
+                if (STAMPS)
+                    acc[EC_TOKENS] += cnt;
+                ESTAMP(EP_TOK);
+                while (tp + cnt - cons_seen > kTok) {    // the emit wave always drains
+                    __builtin_amdgcn_s_sleep(2);
+                    cons_seen = lds_load(&S.cons);
                 }
+                ESTAMP(EP_PUSHWAIT);
+                const uint64_t below = (1ull << l) - 1;
+                if ((km >> l) & 1ull) {
+                    const uint64_t stop = ~(path & ~mstart) & below;
+                    const uint32_t from = stop ? ip + 64 - (uint32_t)__builtin_clzll(stop) : ii;
+                    const uint32_t r = (uint32_t)__builtin_popcountll(km & below);
+                    S.tok[(tp + r) % kTok] = make_uint4(from, p - from, mlen, p - cand);
+                }
+                tp += cnt;
+                lds_store(&S.prod, tp);
+                const uint32_t last = 63 - (uint32_t)__builtin_clzll(km);
+                ii = ip + last + lane_read(mlen, last);
             }
             // UPDATE_I of every path lane before the cut; their slots are distinct
             ESTAMP(EP_TOK);
@@ -391,6 +419,9 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             ip += end;
             if (ip >= ip_end)
                 break;
+#pragma unroll
+            for (int i = 0; i < kCmpW; i++)
+                pw[i] = npw[i];
         }
     }
     push(ii, n - ii, 0, 0);                          // tail + EOF
