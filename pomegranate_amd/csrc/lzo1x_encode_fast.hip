@@ -10,11 +10,12 @@
 //    lane probes its own position against the dictionary as it was before the
 //    window (u16 positions in LDS, 0 = empty: the reference never stores
 //    position 0).  A lane's probe is exact as long as no earlier lane of the
-//    window that really probes writes a slot it reads; lanes set their two
-//    slots' bits in a claim bitmap with ds_or_rtn, and of any two lanes that
-//    share a slot at least one sees the other's bit, so cutting the window
-//    at the first lane that saw one keeps every lane before it exact (lane 0
-//    may be that lane -- the window then holds lane 0 alone).  Within
+//    window that really probes writes a slot it reads.  Path lanes post
+//    (window tag, lane) for the slot they write into a claim table with
+//    ds_min, then read back the entries of the slots they read: an entry of
+//    this window from a lower lane is such a write (or, rarely, another slot
+//    hashing to the same entry), and the window is cut at the first lane that
+//    finds one, so every lane before it is exact.  Within
 //    the exact prefix the greedy parse proceeds as the reference does: the
 //    first matching lane emits a match, the lanes it covers are skipped (they
 //    neither probe nor update the dictionary), and the lane right after it
@@ -45,6 +46,7 @@ constexpr uint32_t kSlots = emit::kSlots;
 constexpr uint32_t kRebase = 8192;
 constexpr uint32_t kMaxN = 1u << 24;            // larger blocks: the general encoder
 constexpr uint32_t kTok = 128;                  // token queue entries
+constexpr uint32_t kClaim = 512;                // claim table entries (slots hashed)
 constexpr uint32_t kStage = 2048;               // emitter output ring
 constexpr uint32_t kM2MaxOffset = 0x800;        // lib/minilzo.c M2_MAX_OFFSET
 constexpr uint32_t kNoLane = 0xFFFFFFFFu;
@@ -58,7 +60,7 @@ constexpr uint32_t kM4MaxOffset = 0xBFFF;       // M4_MAX_OFFSET
 
 struct __attribute__((aligned(16))) EncLds {
     uint16_t dict[kSlots];          // last probe position per hash slot: position - base + 1 (0 = empty)
-    uint32_t claim[kSlots / 32];    // per-window slot claims, cleared after each window
+    uint32_t claim[kClaim];         // (window tag << 8 | lowest writing lane) per hashed slot
     uint4 tok[kTok];                // {literal start, literal count, match length (0: tail), offset}
     uint8_t stage[kStage];          // emitter output ring
     uint32_t prod;                  // tokens published by the parse wave
@@ -70,6 +72,7 @@ struct __attribute__((aligned(16))) EncLds {
 static_assert(sizeof(EncLds) * 4 <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ uint32_t lane_id() { return emit::lane(); }
+__device__ __forceinline__ uint32_t claim_index(uint32_t slot) { return (slot ^ (slot >> 9)) & (kClaim - 1); }
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ void wave_order() { emit::order(); }
@@ -171,7 +174,7 @@ __device__ uint32_t extend_match(const BlockSrc& B, uint32_t n, uint32_t mc, uin
 // Diagnostic build only (STAMPS): per-phase s_memtime cycle sums and counts of
 // the parse wave go to stamps[b * kEncStampSlots + i]; no output depends on them.
 enum { EP_SETUP, EP_PROBE, EP_CAND, EP_PATH, EP_CLAIM, EP_TOK, EP_DICT, EP_PUSHWAIT,
-       EC_WINDOWS, EC_EXTEND, EC_TOKENS, EP_N };
+       EC_WINDOWS, EC_EXTEND, EC_TOKENS, EC_PATHIT, EC_EXTIT, EC_C2NEED, EC_C2MATCH, EP_N };
 constexpr int kEncStampSlots = 16;
 
 template <bool STAMPS>
@@ -208,12 +211,13 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
     if (n > 13) {                                   // lib/minilzo.c:3167-3173
         for (uint32_t s = l; s < kSlots / 2; s += kWave)
             ((uint32_t*)S.dict)[s] = 0;             // zero-filled wrkmem: all EMPTY
-        for (uint32_t s = l; s < kSlots / 32; s += kWave)
-            S.claim[s] = 0;
+        for (uint32_t s = l; s < kClaim; s += kWave)
+            S.claim[s] = 0xFFFFFFFFu;               // (tag 0xFFFFFF: no window has it)
         wave_order();
         const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
         uint32_t ip = 4;
         uint32_t base = 0;                          // dictionary position base
+        uint32_t wtag = 0xFFFFFEu;                  // claim tag of the window (one per window, > 0)
         // Probe words of the window (position ip + l): the next window's are
         // read as soon as its start is known, ahead of the token and
         // dictionary writes.
@@ -294,11 +298,19 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             // lane is a literal.  Lanes inside matches neither probe nor
             // update the dictionary (:3051-3150).
             const uint64_t okm = wave_ballot(ok);
+            if (STAMPS) {
+                __builtin_amdgcn_s_waitcnt(0);       // (attribute the candidate loads here)
+                const bool need2 = v1 && v2 && !(p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
+                acc[EC_C2NEED] += wave_ballot(need2) != 0;
+                acc[EC_C2MATCH] += wave_ballot(ok && slot == h2) != 0;
+            }
             ESTAMP(EP_CAND);
             uint64_t path = 0, mstart = 0;
             uint32_t end = 0;                        // lane where the path leaves the window
             uint32_t deferred = kNoLane;             // a match left unextended: it leaves the window anyway
             while (end < nact) {
+                if (STAMPS)
+                    acc[EC_PATHIT] += 1;
                 const uint64_t rest = okm & (~0ull << end);
                 const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
                 const uint32_t lit_end = q < nact ? q : nact;
@@ -320,6 +332,8 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                     if (STAMPS)
                         acc[EC_EXTEND] += 1;
                     len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
+                    if (STAMPS)
+                        acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
                     mlen = l == q ? len : mlen;
                 }
                 end = q + len;
@@ -327,31 +341,26 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
 
             ESTAMP(EP_PATH);
             // ---- exactness: claims among the path lanes only ------------------
-            // Path lane l reads its two slots and writes one of them.  Of two
-            // path lanes sharing a slot at least one sees the other's bit
-            // (same-address LDS atomics of a wave serialise), so every path
-            // lane before the first lane that saw one is exact; lane 0 always
-            // is.
+            // Path lane l read h1 (and h2 when slot is h2) and writes slot.
+            // The table keeps, per hashed slot, the lowest lane of this window
+            // writing it (ds_min of tag|lane; a wave's LDS operations complete
+            // in order, so the reads below see every post).  A path lane is
+            // inexact only if a lower path lane writes a slot it read.
             const bool onpath = (path >> l) & 1ull;
+            const uint32_t mine = (wtag << 8) | l;
+            if (onpath)
+                atomicMin(&S.claim[claim_index(slot)], mine);
+            wave_order();
             bool conflicted = false;
             if (onpath) {
-                const uint32_t m1 = 1u << (h1 & 31), m2 = 1u << (h2 & 31);
-                const uint32_t o1 = atomicOr(&S.claim[h1 >> 5], m1);
-                const uint32_t o2 = atomicOr(&S.claim[h2 >> 5], m2);
-                conflicted = (o1 & m1) != 0 || (o2 & m2) != 0;
+                const uint32_t t1 = S.claim[claim_index(h1)];
+                const uint32_t t2 = S.claim[claim_index(h2)];
+                conflicted = ((t1 >> 8) == wtag && (t1 & 0xFFu) < l) ||
+                             (slot == h2 && (t2 >> 8) == wtag && (t2 & 0xFFu) < l);
             }
-            wave_order();
-            if (onpath) {
-                S.claim[h1 >> 5] = 0;
-                S.claim[h2 >> 5] = 0;
-            }
-            wave_order();
+            wtag--;
             const uint64_t cm = wave_ballot(conflicted);
-            uint32_t cut = cm ? (uint32_t)__builtin_ctzll(cm) : 0xFFFFFFFFu;
-            if (cut == 0) {                          // lane 0 alone: cut at its path successor
-                const uint64_t succ = path & ~1ull;
-                cut = succ ? (uint32_t)__builtin_ctzll(succ) : end;
-            }
+            uint32_t cut = cm ? (uint32_t)__builtin_ctzll(cm) : 0xFFFFFFFFu;   // never lane 0
 #ifdef POM_ENC_MAXLANES
             cut = cut < POM_ENC_MAXLANES ? cut : POM_ENC_MAXLANES;   // (debugging: a path lane)
             while (cut < 64 && !((path >> cut) & 1ull))
