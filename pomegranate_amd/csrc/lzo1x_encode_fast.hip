@@ -45,9 +45,18 @@ constexpr uint32_t kSlots = emit::kSlots;
 // (lib/minilzo.c:2878-2883) and the parse is unchanged.
 constexpr uint32_t kRebase = 8192;
 constexpr uint32_t kMaxN = 1u << 24;            // larger blocks: the general encoder
-constexpr uint32_t kTok = 128;                  // token queue entries
-constexpr uint32_t kClaim = 512;                // claim table entries (slots hashed)
-constexpr uint32_t kStage = 2048;               // emitter output ring
+#ifndef POM_ENC_TOK
+#define POM_ENC_TOK 64
+#endif
+#ifndef POM_ENC_CLAIM
+#define POM_ENC_CLAIM 1024
+#endif
+#ifndef POM_ENC_STAGE
+#define POM_ENC_STAGE 1024
+#endif
+constexpr uint32_t kTok = POM_ENC_TOK;          // token queue entries
+constexpr uint32_t kClaim = POM_ENC_CLAIM;      // claim table entries (slots hashed)
+constexpr uint32_t kStage = POM_ENC_STAGE;      // emitter output ring
 constexpr uint32_t kM2MaxOffset = 0x800;        // lib/minilzo.c M2_MAX_OFFSET
 constexpr uint32_t kNoLane = 0xFFFFFFFFu;
 constexpr uint32_t kM4MaxOffset = 0xBFFF;       // M4_MAX_OFFSET
