@@ -346,10 +346,54 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
 # ---------------------------------------------------------------------------
 # C5: end-to-end ITB write/read with pinned host<->device copies
 # ---------------------------------------------------------------------------
+def _c5_xnet(args, recs, originals, tmps, path, itb, xnet, plain_bytes):
+    """C5 through the xnet wire format: MDS write-back
+    REQs (compress + frame), MDSL parse + append; MDSL read + XNET_RPY_DATA_ITB
+    replies, MDS parse + receive (copy into whole ITBs + in-place decode)."""
+    n = len(recs)
+    dests = [(0x200 + i % 8, i) for i in range(n)]
+    reqs = [(0x11, i, 0x1000 + i) for i in range(n)]
+    wire = bytearray(sum(itb.header_fields(r)[0] + xnet.TX_SIZE for r in recs))
+    bufs = [bytearray(itb.ITB_FULL) for _ in recs]
+    best = None
+    for _ in range(max(1, args.steps // 5)):
+        t0 = time.perf_counter()
+        rc, wl, err = xnet.wb_batch(recs, tmps, dests, 0x11, 1, 3, wire)
+        frames, used = xnet.parse(wire, wl, magic=3)
+        af = itb.AppendFile(path)
+        locs = [af.append(memoryview(wire)[f.offset: f.offset + f.tx.len]) for f in frames]
+        af.close()
+        t1 = time.perf_counter()
+        fd = os.open(path, os.O_RDONLY)
+        stored = [itb.read_record(fd, loc) for loc in locs]
+        os.close(fd)
+        ta = time.perf_counter()
+        rc2, wl2 = xnet.reply_batch(stored, reqs, 0x200, 3, wire)
+        tb = time.perf_counter()
+        frames2, _ = xnet.parse(wire, wl2, magic=3)
+        tc = time.perf_counter()
+        rerr = xnet.recv_batch(wire, frames2, bufs)
+        t2 = time.perf_counter()
+        stages = {"read_ms": round(1e3 * (ta - t1), 2), "reply_ms": round(1e3 * (tb - ta), 2),
+                  "parse_ms": round(1e3 * (tc - tb), 2), "recv_ms": round(1e3 * (t2 - tc), 2)}
+        errors = (rc != 0) + (rc2 != 0) + (used != wl) + sum(1 for e in err if e) + \
+            sum(1 for e in rerr if e) + (len(frames2) != n)
+        for b, o in zip(bufs, originals):
+            h = bytearray(b[: itb.ITBH_SIZE])
+            h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = o[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
+            errors += bytes(h) + bytes(b[itb.ITBH_SIZE: len(o)]) != o
+        cur = (t1 - t0, t2 - t1, errors, wl, stages)
+        if best is None or cur[0] + cur[1] < best[0] + best[1]:
+            best = cur
+    w, r, errors, wl, stages = best
+    return {"write_gibps": round(plain_bytes / w / GIB, 3), "read_gibps": round(plain_bytes / r / GIB, 3),
+            "wire_bytes": int(wl), "messages": n, "errors": errors, "read_stages": stages}
+
+
 def run_c5(args, rank):
     import tempfile
 
-    from pomegranate_amd import itb
+    from pomegranate_amd import itb, xnet
     rng = np.random.default_rng(5)
     ites = rng.integers(1, 1025, args.c5_records)
     recs = [itb.make_record(100000 + i, int(k)) for i, k in enumerate(ites)]
@@ -390,13 +434,14 @@ def run_c5(args, rank):
             if best is None or cur[1] + cur[3] < best[1] + best[3]:
                 best = cur
         c, w, dcd, r, errors, ncomp, fbytes = best
+        xres = _c5_xnet(args, recs, originals, tmps, path, itb, xnet, plain_bytes)
         res = {"records": len(recs), "uncompressed_bytes": int(plain_bytes),
                "file_bytes": fbytes, "compressed_records": ncomp,
                "write_gibps": round(plain_bytes / w / GIB, 3),
                "read_gibps": round(plain_bytes / r / GIB, 3),
                "compress_pcie_gibps": round(plain_bytes / c / GIB, 3),
                "decompress_pcie_gibps": round(plain_bytes / dcd / GIB, 3),
-               "errors": errors}
+               "errors": errors + xres["errors"], "xnet": xres}
     finally:
         if os.path.exists(path):
             os.unlink(path)

@@ -1,0 +1,188 @@
+/*
+ * xnet_frame.c -- xnet wire framing of ITB messages over the ITB codec
+ * (include/pom_xnet.h).
+ *
+ *   frame / parse  struct xnet_msg_tx + tx.len data bytes, the magic check
+ *                  (include/xnet.h:27-67, xnet/xnet_simple.c:480-587, :1912)
+ *   reply          __mdsl_send_rpy_data with flag 1 (mdsl/m2ml.c:87-120)
+ *   write-back     txg_wb_itb: compress, then the REQ (mds/txg.c:548-584, :733-770)
+ *   receive        the MDS load path (mds/itb.c:140-168, test/xnet/mds.c:683-691)
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "minilzo.h"
+#include "pom_itb.h"
+#include "pom_xnet.h"
+
+_Static_assert(sizeof(struct pom_xnet_tx) == POM_XNET_TX_SIZE, "struct xnet_msg_tx is 72 bytes");
+
+static uint32_t rd32(const uint8_t *p)
+{
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v;
+}
+
+static uint16_t rd16(const uint8_t *p)
+{
+    uint16_t v;
+    memcpy(&v, p, 2);
+    return v;
+}
+
+size_t pom_xnet_frame(uint8_t *wire, size_t cap, const struct pom_xnet_tx *hdr,
+                      const void *data, uint32_t len)
+{
+    const size_t need = POM_XNET_TX_SIZE + (size_t)len;
+    if (cap < need)
+        return 0;
+    struct pom_xnet_tx tx = *hdr;
+    tx.len = len;
+    memcpy(wire, &tx, POM_XNET_TX_SIZE);
+    if (len)
+        memcpy(wire + POM_XNET_TX_SIZE, data, len);
+    return need;
+}
+
+int pom_xnet_parse(const uint8_t *wire, size_t len, uint8_t magic, struct pom_xnet_frame *f,
+                   size_t max, size_t *nframes, size_t *consumed)
+{
+    size_t off = 0, nf = 0;
+    magic &= 15u;                                   /* a 4-bit field on the wire */
+    while (nf < max && len - off >= POM_XNET_TX_SIZE) {
+        struct pom_xnet_tx tx;
+        memcpy(&tx, wire + off, POM_XNET_TX_SIZE);
+        if (len - off - POM_XNET_TX_SIZE < tx.len)
+            break;                                  /* data not all here yet */
+        f[nf].tx = tx;
+        f[nf].data = wire + off + POM_XNET_TX_SIZE;
+        /* our magic 0 accepts all, and so does a message without one */
+        f[nf].dropped = magic && POM_XNET_MAGIC(tx) && POM_XNET_MAGIC(tx) != magic;
+        off += POM_XNET_TX_SIZE + tx.len;
+        nf++;
+    }
+    *nframes = nf;
+    *consumed = off;
+    return 0;
+}
+
+static struct pom_xnet_tx header(uint8_t type, uint16_t flag, uint64_t ssite, uint64_t dsite,
+                                 uint8_t magic)
+{
+    struct pom_xnet_tx tx;
+    memset(&tx, 0, sizeof(tx));                     /* xnet_alloc_msg zero-fills */
+    tx.vm = (uint8_t)((magic & 15u) << 4);          /* version stays 0 */
+    tx.type = type;                                 /* xnet_msg_fill_tx */
+    tx.flag = flag;
+    tx.ssite_id = ssite;
+    tx.dsite_id = dsite;
+    return tx;
+}
+
+int pom_xnet_itb_reply_batch(const uint8_t *const *itb, const struct pom_xnet_req *req, size_t n,
+                             uint64_t site_id, uint8_t magic, uint8_t *wire, size_t cap,
+                             size_t *wire_len)
+{
+    size_t off = 0;
+    *wire_len = 0;
+    for (size_t b = 0; b < n; b++) {
+        struct pom_xnet_tx tx = header(POM_XNET_MSG_RPY, POM_XNET_NEED_DATA_FREE, site_id,
+                                       req[b].ssite_id, magic);
+        tx.reqno = req[b].reqno;                    /* xnet_msg_fill_reqno */
+        tx.cmd = POM_XNET_RPY_DATA_ITB;             /* xnet_msg_fill_cmd(rpy, ..., 0, 0) */
+        tx.handle = req[b].handle;                  /* match the request at its source */
+        const size_t w = pom_xnet_frame(wire + off, cap - off, &tx, itb[b],
+                                        rd32(itb[b] + POM_ITBH_LEN_OFF));
+        if (!w)
+            return -ENOSPC;
+        off += w;
+        *wire_len = off;
+    }
+    return 0;
+}
+
+int pom_xnet_itb_wb_batch(uint8_t *const *itb, uint8_t *const *tmp, const size_t *tmp_cap,
+                          const struct pom_xnet_wb *wb, size_t n, uint64_t site_id, uint64_t txg,
+                          uint8_t magic, uint8_t *wire, size_t cap, size_t *wire_len, int *err)
+{
+    *wire_len = 0;
+    if (n == 0)
+        return 0;
+    uint8_t **oi = malloc(n * sizeof(*oi));
+    if (!oi)
+        return LZO_E_OUT_OF_MEMORY;
+    int rc = pom_itb_lzo_compress_batch(itb, tmp, tmp_cap, oi, err, n);
+    if (rc == LZO_E_OK) {
+        size_t off = 0;
+        for (size_t b = 0; b < n; b++) {
+            const uint8_t *rec = err[b] ? itb[b] : oi[b];
+            struct pom_xnet_tx tx = header(POM_XNET_MSG_REQ, 0, site_id, wb[b].dsite_id, magic);
+            tx.cmd = POM_HVFS_MDS2MDSL_WBTXG;       /* xnet_msg_fill_cmd(msg, WBTXG, ITB, txg) */
+            tx.arg0 = POM_HVFS_WBTXG_ITB;
+            tx.arg1 = txg;
+            tx.reserved = wb[b].vid;
+            const size_t w = pom_xnet_frame(wire + off, cap - off, &tx, rec,
+                                            rd32(rec + POM_ITBH_LEN_OFF));
+            if (!w) {
+                rc = -ENOSPC;
+                break;
+            }
+            off += w;
+            *wire_len = off;
+        }
+    }
+    free(oi);
+    return rc;
+}
+
+int pom_xnet_itb_recv_batch(const struct pom_xnet_frame *f, size_t n, uint8_t *const *itb,
+                            size_t itb_cap, int *err)
+{
+    if (n == 0)
+        return 0;
+    uint8_t **dec = malloc(n * sizeof(*dec));
+    size_t *cap = malloc(n * sizeof(*cap));
+    size_t *at = malloc(n * sizeof(*at));
+    int *derr = malloc(n * sizeof(*derr));
+    int rc = LZO_E_OUT_OF_MEMORY;
+    if (!dec || !cap || !at || !derr)
+        goto out;
+    size_t nd = 0;
+    for (size_t b = 0; b < n; b++) {
+        err[b] = 0;
+        if (f[b].dropped) {
+            err[b] = -EBADMSG;
+            continue;
+        }
+        const uint32_t len = f[b].tx.len;
+        if (len < POM_ITBH_SIZE || len > itb_cap) {
+            err[b] = -EIO;
+            continue;
+        }
+        memcpy(itb[b], f[b].data, len);
+        if (rd32(itb[b] + POM_ITBH_LEN_OFF) != len) {   /* the load path's ASSERT */
+            err[b] = -EIO;
+            continue;
+        }
+        if (rd16(itb[b] + POM_ITBH_ALGO_OFF) == POM_COMPR_LZO) {
+            dec[nd] = itb[b];
+            cap[nd] = itb_cap;
+            at[nd] = b;
+            nd++;
+        }
+    }
+    rc = pom_itb_lzo_decompress_batch(dec, cap, derr, NULL, nd);
+    if (rc != LZO_E_OK)
+        goto out;
+    for (size_t i = 0; i < nd; i++)
+        if (derr[i] != LZO_E_OK)
+            err[at[i]] = -EFAULT;                   /* itb_lzo_decompress failed */
+out:
+    free(dec);
+    free(cap);
+    free(at);
+    free(derr);
+    return rc;
+}

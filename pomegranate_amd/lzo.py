@@ -50,6 +50,9 @@ EXPORTS = (
     "pom_abuf_open", "pom_abuf_append", "pom_abuf_close", "pom_itb_read",
     # include/pom_column.h
     "pom_col_zip_bound", "pom_col_zip_batch", "pom_col_zipv", "pom_col_unzip_batch",
+    # include/pom_xnet.h
+    "pom_xnet_frame", "pom_xnet_parse", "pom_xnet_itb_reply_batch", "pom_xnet_itb_wb_batch",
+    "pom_xnet_itb_recv_batch",
 )
 
 _lib: Optional[ctypes.CDLL] = None
