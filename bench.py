@@ -346,7 +346,7 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
 # ---------------------------------------------------------------------------
 # C5: end-to-end ITB write/read with pinned host<->device copies
 # ---------------------------------------------------------------------------
-def _c5_xnet(args, recs, originals, tmps, path, itb, xnet, plain_bytes):
+def _c5_xnet(args, recs, originals, tmps, rbufs, path, itb, xnet, plain_bytes):
     """C5 through the xnet wire format: MDS write-back
     REQs (compress + frame), MDSL parse + append; MDSL read + XNET_RPY_DATA_ITB
     replies, MDS parse + receive (copy into whole ITBs + in-place decode)."""
@@ -365,7 +365,7 @@ def _c5_xnet(args, recs, originals, tmps, path, itb, xnet, plain_bytes):
         af.close()
         t1 = time.perf_counter()
         fd = os.open(path, os.O_RDONLY)
-        stored = [itb.read_record(fd, loc) for loc in locs]
+        stored = [itb.read_record(fd, loc, out=b) for loc, b in zip(locs, rbufs)]
         os.close(fd)
         ta = time.perf_counter()
         rc2, wl2 = xnet.reply_batch(stored, reqs, 0x200, 3, wire)
@@ -400,6 +400,7 @@ def run_c5(args, rank):
     plain_bytes = float(sum(itb.header_fields(r)[0] - itb.ITBH_SIZE for r in recs))
     originals = [bytes(r[: itb.header_fields(r)[0]]) for r in recs]
     tmps = [bytearray(itb.ITB_FULL) for _ in recs]
+    rbufs = [bytearray(itb.ITB_FULL) for _ in recs]             # read buffers (whole ITBs), reused
     itb.compress_batch(recs[:4], tmps[:4])                      # warm-up (context, staging)
     d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
     path = os.path.join(d, f"pom_c5_{os.getpid()}_{rank}.itb")
@@ -416,7 +417,7 @@ def run_c5(args, rank):
             af.close()
             t2 = time.perf_counter()
             fd = os.open(path, os.O_RDONLY)
-            back = [itb.read_record(fd, loc) for loc in locs]
+            back = [itb.read_record(fd, loc, out=b) for loc, b in zip(locs, rbufs)]
             os.close(fd)
             t3 = time.perf_counter()
             comp_idx = [i for i, b in enumerate(back) if itb.header_fields(b)[2] == itb.COMPR_LZO]
@@ -434,7 +435,7 @@ def run_c5(args, rank):
             if best is None or cur[1] + cur[3] < best[1] + best[3]:
                 best = cur
         c, w, dcd, r, errors, ncomp, fbytes = best
-        xres = _c5_xnet(args, recs, originals, tmps, path, itb, xnet, plain_bytes)
+        xres = _c5_xnet(args, recs, originals, tmps, rbufs, path, itb, xnet, plain_bytes)
         res = {"records": len(recs), "uncompressed_bytes": int(plain_bytes),
                "file_bytes": fbytes, "compressed_records": ncomp,
                "write_gibps": round(plain_bytes / w / GIB, 3),

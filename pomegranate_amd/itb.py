@@ -141,9 +141,12 @@ class AppendFile:
             raise OSError(-rc, os.strerror(-rc))
 
 
-def read_record(fd: int, location: int, cap: int = ITB_FULL) -> bytearray:
+def read_record(fd: int, location: int, cap: int = ITB_FULL,
+                out: "bytearray | None" = None) -> bytearray:
+    """pom_itb_read into `out` (reused, len(out) is the cap) or a new buffer."""
     lib = _lib()
-    buf = bytearray(cap)
+    buf = bytearray(cap) if out is None else out
+    cap = len(buf)
     c = (ctypes.c_char * cap).from_buffer(buf)
     ln = ctypes.c_size_t(0)
     rc = lib.pom_itb_read(fd, location, ctypes.addressof(c), cap, ctypes.byref(ln))
