@@ -538,6 +538,27 @@ __global__ __launch_bounds__(kWave) void lzo1x_encode_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Pack: each block's produced bytes (min(len, cap)) from its capacity-sized
+// slot to consecutive 16-byte-aligned offsets, so the host batch path copies
+// back only what the kernels produced.  Slots and offsets are 16-B aligned
+// and padded, so whole 16-byte granules are copied.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_kernel(const uint8_t* __restrict__ from,
+                                                   const uint64_t* __restrict__ from_off,
+                                                   const uint32_t* __restrict__ len,
+                                                   const uint32_t* __restrict__ cap,
+                                                   const uint64_t* __restrict__ to_off,
+                                                   uint8_t* __restrict__ to)
+{
+    const uint32_t b = blockIdx.x;
+    const uint32_t n = len[b] < cap[b] ? len[b] : cap[b];
+    const uint4* s = (const uint4*)(from + from_off[b]);
+    uint4* d = (uint4*)(to + to_off[b]);
+    for (uint32_t i = threadIdx.x; i < (n + 15u) / 16u; i += blockDim.x)
+        d[i] = s[i];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -584,5 +605,17 @@ extern "C" int lzo_mi355x_launch_decoded_length(const uint8_t* src, const uint64
     hipLaunchKernelGGL(lzo1x_decode_exact_kernel<false>, dim3(nblocks), dim3(kWave), 0, stream,
                        src, src_off, src_len, nullptr, nullptr, nullptr, out_len, status,
                        nullptr, nblocks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzo_mi355x_launch_pack(const uint8_t* from, const uint64_t* from_off,
+                                      const uint32_t* len, const uint32_t* cap,
+                                      const uint64_t* to_off, uint8_t* to, uint32_t nblocks,
+                                      hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(pack_kernel, dim3(nblocks), dim3(256), 0, stream, from, from_off, len, cap,
+                       to_off, to);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

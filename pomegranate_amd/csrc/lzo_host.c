@@ -270,11 +270,16 @@ static void copy_jobs(const struct copy_job *jobs, size_t n)
 
 /* Staging layout (identical on host and device, so one copy each way):
  *   [src_off u64][dst_off u64][src_len u32][dst_cap u32][out_len u32][status i32]
- *   [src bytes, 16-B aligned per block][dst bytes, 16-B aligned per block] */
+ *   [packed offset u64]
+ *   [src bytes, 16-B aligned per block][dst bytes, 16-B aligned per block]
+ *   [decoder scratch]  [device only: packed output]
+ * The kernels write each block into its capacity-sized dst slot; only the
+ * produced bytes come back, packed (pack kernel), in one D2H copy into the
+ * host's dst region. */
 struct layout {
     size_t nb;
-    size_t o_srcoff, o_dstoff, o_srclen, o_dstcap, o_outlen, o_status;
-    size_t o_src, o_dst, o_scr, total;
+    size_t o_srcoff, o_dstoff, o_srclen, o_dstcap, o_outlen, o_status, o_poff;
+    size_t o_src, o_dst, o_scr, o_pack, total, dtotal;
     size_t src_bytes, dst_bytes;
 };
 
@@ -288,6 +293,7 @@ static void layout_make(struct layout *L, size_t nb, const size_t *src_len, cons
     L->o_dstcap = o; o += 4 * nb;
     L->o_outlen = o; o += 4 * nb;
     L->o_status = o; o += 4 * nb;
+    L->o_poff = o; o += 8 * nb;
     o = ALIGN_UP(o, 256);
     L->o_src = o;
     size_t s = 0, d = 0;
@@ -303,6 +309,8 @@ static void layout_make(struct layout *L, size_t nb, const size_t *src_len, cons
     L->o_scr = o;
     o += ALIGN_UP(lzo_mi355x_decompress_scratch((uint32_t)nb), 256);
     L->total = o;
+    L->o_pack = o;
+    L->dtotal = o + ALIGN_UP(d, 256);
 }
 
 static void layout_fill(const struct layout *L, uint8_t *h, const uint8_t *const *src,
@@ -362,11 +370,27 @@ static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
     if (rc != 0)
         return -1;
     if (hipMemcpyAsync(h + L->o_outlen, d + L->o_outlen, 8 * L->nb, hipMemcpyDeviceToHost, s) !=
-        hipSuccess)
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
         return -1;
-    if (L->dst_bytes &&
-        hipMemcpyAsync(h + L->o_dst, d + L->o_dst, L->dst_bytes, hipMemcpyDeviceToHost, s) !=
-            hipSuccess)
+    /* packed offsets of the produced bytes, then one copy of exactly those */
+    const uint32_t *hol = (const uint32_t *)(h + L->o_outlen);
+    const uint32_t *hdc = (const uint32_t *)(h + L->o_dstcap);
+    uint64_t *poff = (uint64_t *)(h + L->o_poff);
+    size_t packed = 0;
+    for (size_t b = 0; b < L->nb; b++) {
+        poff[b] = packed;
+        packed += ALIGN_UP((size_t)(hol[b] < hdc[b] ? hol[b] : hdc[b]), 16);
+    }
+    if (packed == 0)
+        return 0;
+    if (hipMemcpyAsync(d + L->o_poff, poff, 8 * L->nb, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -1;
+    if (lzo_mi355x_launch_pack(d + L->o_dst, dof, ol, dc, (const uint64_t *)(d + L->o_poff),
+                               d + L->o_pack, nb, s) != 0)
+        return -1;
+    if (hipMemcpyAsync(h + L->o_dst, d + L->o_pack, packed, hipMemcpyDeviceToHost, s) !=
+        hipSuccess)
         return -1;
     return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
 }
@@ -396,21 +420,21 @@ static int batch_common(enum op_kind kind, const uint8_t *const *src, const size
     struct layout L;
     layout_make(&L, nblocks, src_len, cap);
     int rc = LZO_E_ERROR;
-    if (tctx_reserve(t, L.total, L.total) == 0) {
+    if (tctx_reserve(t, L.dtotal, L.total) == 0) {
         layout_fill(&L, t->hmem, src, src_len, cap);
         if (run_staged(t, &L, kind) == 0) {
             const uint32_t *ol = (const uint32_t *)(t->hmem + L.o_outlen);
             const int32_t *st = (const int32_t *)(t->hmem + L.o_status);
-            const uint64_t *dof = (const uint64_t *)(t->hmem + L.o_dstoff);
+            const uint64_t *poff = (const uint64_t *)(t->hmem + L.o_poff);
             struct copy_job *jobs = malloc(nblocks * sizeof(*jobs));
             for (size_t b = 0; b < nblocks; b++) {
                 size_t n = ol[b] < cap[b] ? ol[b] : cap[b];
                 if (jobs) {
                     jobs[b].dst = dst[b];
-                    jobs[b].src = t->hmem + L.o_dst + dof[b];
+                    jobs[b].src = t->hmem + L.o_dst + poff[b];
                     jobs[b].len = n;
                 } else if (n) {
-                    memcpy(dst[b], t->hmem + L.o_dst + dof[b], n);
+                    memcpy(dst[b], t->hmem + L.o_dst + poff[b], n);
                 }
                 dst_len[b] = ol[b];
                 status[b] = st[b];
