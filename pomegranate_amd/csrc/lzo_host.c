@@ -395,9 +395,25 @@ static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
     return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
 }
 
+/* POM_HOST_TIMING=1: per-phase wall times of each host batch on stderr (diagnostic) */
+static double now_ms(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
 static int batch_common(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
                         uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks)
 {
+    static int timing = -1;
+    if (timing < 0) {
+        const char *e = getenv("POM_HOST_TIMING");
+        timing = e && *e == '1';
+    }
+    double tm[5] = {0};
+    if (timing)
+        tm[0] = now_ms();
     struct tctx *t = tctx_get();
     if (!t)
         return LZO_E_ERROR;
@@ -421,8 +437,14 @@ static int batch_common(enum op_kind kind, const uint8_t *const *src, const size
     layout_make(&L, nblocks, src_len, cap);
     int rc = LZO_E_ERROR;
     if (tctx_reserve(t, L.dtotal, L.total) == 0) {
+        if (timing)
+            tm[1] = now_ms();
         layout_fill(&L, t->hmem, src, src_len, cap);
+        if (timing)
+            tm[2] = now_ms();
         if (run_staged(t, &L, kind) == 0) {
+            if (timing)
+                tm[3] = now_ms();
             const uint32_t *ol = (const uint32_t *)(t->hmem + L.o_outlen);
             const int32_t *st = (const int32_t *)(t->hmem + L.o_status);
             const uint64_t *poff = (const uint64_t *)(t->hmem + L.o_poff);
@@ -444,6 +466,12 @@ static int batch_common(enum op_kind kind, const uint8_t *const *src, const size
                 free(jobs);
             }
             rc = LZO_E_OK;
+            if (timing) {
+                tm[4] = now_ms();
+                fprintf(stderr, "pom host %s n=%zu: reserve %.2f pack %.2f gpu %.2f unpack %.2f ms\n",
+                        kind == OP_COMPRESS ? "compress" : "decompress", nblocks, tm[1] - tm[0],
+                        tm[2] - tm[1], tm[3] - tm[2], tm[4] - tm[3]);
+            }
         }
     }
     free(cap);

@@ -138,11 +138,10 @@ def _adversarial_blocks():
     """Inputs aimed at the throughput encoder's windowing
     (lzo1x_encode_fast.hip): short periods (every lane of a window hashes to
     the same few slots), periods around the 64-lane window, 4-byte patterns
-    that collide in the 16384-slot dictionary, long matches (the 16-byte
-    speculative compare and the wave-parallel extension), matches running
-    into the block end, sizes around the 64 KiB u16-position limit (65536
-    takes the fast kernel, 65537 the general one), and the 14..17-byte blocks
-    whose first probe lies at or past ip_end."""
+    that collide in the 16384-slot dictionary, long matches (the 32-byte
+    first compare and the wave-parallel extension), matches running into the
+    block end, sizes around 64 KiB (where the u16 dictionary first re-bases),
+    and the 14..17-byte blocks whose first probe lies at or past ip_end."""
     rng = np.random.default_rng(11)
     out = []
     for period in (1, 2, 3, 4, 5, 7, 8, 13, 31, 32, 33, 63, 64, 65, 67, 127, 128, 129, 255):
@@ -168,8 +167,44 @@ def _adversarial_blocks():
     return out
 
 
+def _slot_primary(w):
+    b0, b1, b2, b3 = w & 255, (w >> 8) & 255, (w >> 16) & 255, w >> 24
+    v = ((((b3 << 6) ^ b2) << 5) ^ b1)
+    v = (v << 5) ^ b0
+    return ((v * 33) >> 5) & 0x3FFF
+
+
+def _claim_blocks():
+    """Inputs aimed at the encoder's claim table and token writes:
+    words whose dictionary slots differ but share a claim-table entry
+    ((slot ^ slot >> 9) & 1023: aliases cut windows early, never wrongly);
+    windows full of 3-5 byte matches (many tokens per window, token-queue
+    back-pressure); and blocks past 64 KiB with repeats at distances
+    0xBFFF / 0xC000 across the dictionary re-bases (every 8 KiB)."""
+    rng = np.random.default_rng(23)
+    words = rng.integers(0, 2**32, 20000, dtype=np.uint64).astype(np.uint32)
+    groups = {}
+    for w in words.tolist():
+        s = _slot_primary(w)
+        groups.setdefault((s ^ (s >> 9)) & 1023, {}).setdefault(s, w)
+    alias = max(groups.values(), key=len)            # distinct slots, one claim entry
+    aw = np.array(list(alias.values()), dtype=np.uint32)
+    out = [aw[rng.integers(0, len(aw), 16384)].tobytes()]
+    # many short matches: a 5-byte motif with one varying byte
+    motif = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+    out.append(b"".join(motif[:3] + bytes([int(x)]) + motif[3:] for x in rng.integers(0, 7, 13000)))
+    for n in (90000, 200000):
+        d = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        for dist in (0xBFFE, 0xBFFF, 0xC000, 0xC001):
+            for at in range(dist + 5, n - 300, 24571):
+                L = int(rng.integers(3, 200))
+                d[at: at + L] = d[at - dist: at - dist + L]
+        out.append(bytes(d))
+    return out
+
+
 def test_encoder_adversarial_vs_oracle(dev, gu, oracle):
-    blocks = _adversarial_blocks()
+    blocks = _adversarial_blocks() + _claim_blocks()
     comps, st = gu.gpu_compress(torch, blocks, dev, shift=3)
     assert all(s == 0 for s in st)
     for i, (b, c) in enumerate(zip(blocks, comps)):
