@@ -137,6 +137,9 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 #ifndef POM_ENC_CMP
 #define POM_ENC_CMP 8                            // dwords compared in the window round trip
 #endif
+#ifndef POM_ENC_PATHMAX
+#define POM_ENC_PATHMAX 4                        // matches the path walk takes per window
+#endif
 #ifndef POM_ENC_DEFER
 #define POM_ENC_DEFER 0                          // extend a match leaving the window after the cut
 #endif
@@ -317,6 +320,7 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             uint64_t path = 0, mstart = 0;
             uint32_t end = 0;                        // lane where the path leaves the window
             uint32_t deferred = kNoLane;             // a match left unextended: it leaves the window anyway
+            uint32_t nmatch = 0;
             while (end < nact) {
                 if (STAMPS)
                     acc[EC_PATHIT] += 1;
@@ -346,6 +350,8 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                     mlen = l == q ? len : mlen;
                 }
                 end = q + len;
+                if (++nmatch >= POM_ENC_PATHMAX)     // the window ends after this match
+                    break;
             }
 
             ESTAMP(EP_PATH);
