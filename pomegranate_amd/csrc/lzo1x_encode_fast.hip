@@ -68,9 +68,11 @@ constexpr uint32_t kM4MaxOffset = 0xBFFF;       // M4_MAX_OFFSET
 #endif
 
 struct __attribute__((aligned(16))) EncLds {
-    uint16_t dict[kSlots];          // last probe position per hash slot: position - base + 1 (0 = empty)
-    uint32_t claim[kClaim];         // (window tag << 8 | lowest writing lane) per hashed slot
-    uint4 tok[kTok];                // {literal start, literal count, match length (0: tail), offset}
+    // (each array has one spare entry past its end: the target of the writes
+    // of lanes that take no part, instead of an exec-masked branch)
+    uint16_t dict[kSlots + 2];      // last probe position per hash slot: position - base + 1 (0 = empty)
+    uint32_t claim[kClaim + 1];     // (window tag << 8 | lowest writing lane) per hashed slot
+    uint4 tok[kTok + 1];            // {literal start, literal count, match length (0: tail), offset}
     uint8_t stage[kStage];          // emitter output ring
     uint32_t prod;                  // tokens published by the parse wave
     uint32_t cons;                  // tokens consumed by the emit wave
@@ -256,16 +258,13 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 S.ip = ip;
             const uint32_t p = ip + l;
             const bool active = l == 0 || p < ip_end;   // the first probe always runs
-            uint32_t h1 = 0, h2 = 0, w1 = 0, w2 = 0;
-            if (active) {
-                const uint32_t b0 = pw[0] & 0xFF, b1 = (pw[0] >> 8) & 0xFF;
-                const uint32_t b2 = (pw[0] >> 16) & 0xFF, b3 = pw[0] >> 24;
-                h1 = emit::slot_primary(b0, b1, b2, b3);
-                h2 = emit::slot_secondary(h1);
-                const uint32_t e1 = S.dict[h1], e2 = S.dict[h2];
-                w1 = e1 ? base + e1 - 1 : 0u;           // (positions >= 4: 0 stays "empty")
-                w2 = e2 ? base + e2 - 1 : 0u;
-            }
+            // (every lane probes; an inactive one ends with no candidate)
+            const uint32_t h1 = emit::slot_primary(pw[0] & 0xFF, (pw[0] >> 8) & 0xFF,
+                                                   (pw[0] >> 16) & 0xFF, pw[0] >> 24);
+            const uint32_t h2 = emit::slot_secondary(h1);
+            const uint32_t e1 = S.dict[h1], e2 = S.dict[h2];
+            const uint32_t w1 = active && e1 ? base + e1 - 1 : 0u;   // (positions >= 4: 0 stays "empty")
+            const uint32_t w2 = active && e2 ? base + e2 - 1 : 0u;
             const uint64_t am = wave_ballot(active);
             const uint32_t nact = (uint32_t)__builtin_popcountll(am);
             if (STAMPS)
@@ -280,26 +279,16 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             load_at<kCmpW>(B, w1, c1w);
             load_at<kCmpW>(B, w2, c2w);
             const uint32_t b3 = pw[0] >> 24;
-            bool tm = false;
-            uint32_t slot = h1, cand = w1;
+            // (selects, no branches)
+            const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
+            const bool use2 = v1 && !c1pass;         // the secondary slot is read and written
+            const bool c2pass = use2 && v2 && (p - w2 <= kM2MaxOffset || (c2w[0] >> 24) == b3);
+            const bool tm = c1pass || c2pass;
+            const uint32_t slot = use2 ? h2 : h1, cand = c2pass ? w2 : w1;
             uint32_t cw[kCmpW];
 #pragma unroll
             for (int i = 0; i < kCmpW; i++)
-                cw[i] = c1w[i];
-            if (v1) {
-                if (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3) {
-                    tm = true;
-                } else {
-                    slot = h2;
-                    if (v2 && (p - w2 <= kM2MaxOffset || (c2w[0] >> 24) == b3)) {
-                        tm = true;
-                        cand = w2;
-#pragma unroll
-                        for (int i = 0; i < kCmpW; i++)
-                            cw[i] = c2w[i];
-                    }
-                }
-            }
+                cw[i] = c2pass ? c2w[i] : c1w[i];
             // try_match (:2962-2971), then the match length as far as kCmpB bytes
             const bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
             uint32_t mlen = first_diff<kCmpW>(cw, pw);
@@ -363,16 +352,12 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             // inexact only if a lower path lane writes a slot it read.
             const bool onpath = (path >> l) & 1ull;
             const uint32_t mine = (wtag << 8) | l;
-            if (onpath)
-                atomicMin(&S.claim[claim_index(slot)], mine);
+            atomicMin(&S.claim[onpath ? claim_index(slot) : kClaim], mine);
             wave_order();
-            bool conflicted = false;
-            if (onpath) {
-                const uint32_t t1 = S.claim[claim_index(h1)];
-                const uint32_t t2 = S.claim[claim_index(h2)];
-                conflicted = ((t1 >> 8) == wtag && (t1 & 0xFFu) < l) ||
-                             (slot == h2 && (t2 >> 8) == wtag && (t2 & 0xFFu) < l);
-            }
+            const uint32_t t1 = S.claim[claim_index(h1)];
+            const uint32_t t2 = S.claim[claim_index(h2)];
+            const bool conflicted = onpath && (((t1 >> 8) == wtag && (t1 & 0xFFu) < l) ||
+                                               (use2 && (t2 >> 8) == wtag && (t2 & 0xFFu) < l));
             wtag--;
             const uint64_t cm = wave_ballot(conflicted);
             uint32_t cut = cm ? (uint32_t)__builtin_ctzll(cm) : 0xFFFFFFFFu;   // never lane 0
@@ -421,12 +406,10 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 }
                 ESTAMP(EP_PUSHWAIT);
                 const uint64_t below = (1ull << l) - 1;
-                if ((km >> l) & 1ull) {
-                    const uint64_t stop = ~(path & ~mstart) & below;
-                    const uint32_t from = stop ? ip + 64 - (uint32_t)__builtin_clzll(stop) : ii;
-                    const uint32_t r = (uint32_t)__builtin_popcountll(km & below);
-                    S.tok[(tp + r) % kTok] = make_uint4(from, p - from, mlen, p - cand);
-                }
+                const uint64_t stop = ~(path & ~mstart) & below;
+                const uint32_t from = stop ? ip + 64 - (uint32_t)__builtin_clzll(stop) : ii;
+                const uint32_t r = (uint32_t)__builtin_popcountll(km & below);
+                S.tok[(km >> l) & 1ull ? (tp + r) % kTok : kTok] = make_uint4(from, p - from, mlen, p - cand);
                 tp += cnt;
                 lds_store(&S.prod, tp);
                 const uint32_t last = 63 - (uint32_t)__builtin_clzll(km);
@@ -434,8 +417,7 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             }
             // UPDATE_I of every path lane before the cut; their slots are distinct
             ESTAMP(EP_TOK);
-            if ((path & keep) >> l & 1ull)
-                S.dict[slot] = (uint16_t)(p - base + 1);
+            S.dict[(path & keep) >> l & 1ull ? slot : kSlots] = (uint16_t)(p - base + 1);
             wave_order();
             ESTAMP(EP_DICT);
             if (done)
@@ -520,6 +502,13 @@ __device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out
                 }
                 return;
             }
+#ifdef POM_ENC_NOEMIT
+            if (POM_ENC_NOEMIT) {                    // (timing experiment only: no output)
+                pos += t.y + t.z;
+                lds_store(&S.cons, ct);
+                continue;
+            }
+#endif
             if (!poisoned) {
                 if (t.y) {
                     emit::lit_header(e, t.y);
