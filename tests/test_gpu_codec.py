@@ -284,3 +284,35 @@ def test_decompress_mutated_streams_vs_oracle(dev, gu, oracle):
         if st[i] != rc or outs[i] != want:
             bad.append((i, st[i], rc, len(outs[i]), len(want)))
     assert not bad, bad[:6]
+
+
+def _large_block(n, seed):
+    """ITB-like content with long-distance repeats (the u16 dictionary re-bases
+    every 8 KiB past 64 KiB) and an incompressible stretch."""
+    rng = np.random.default_rng(seed)
+    parts, total = [], 0
+    while total < n:
+        k = int(rng.integers(0, 3))
+        if k == 0:
+            b = synth.block(synth.ITB, int(rng.integers(0, 1 << 30)), 65536)
+        elif k == 1:
+            b = rng.integers(0, 256, 20000, dtype=np.uint8).tobytes()
+        else:
+            ref = b"".join(parts)[-200000:] or b"x" * 64
+            a = int(rng.integers(0, max(1, len(ref) - 5000)))
+            b = ref[a: a + 5000]
+        parts.append(b)
+        total += len(b)
+    return b"".join(parts)[:n]
+
+
+@pytest.mark.parametrize("n", [(3 << 20) + 5, 16 << 20, (16 << 20) + 1])
+def test_large_blocks_vs_oracle(dev, gu, oracle, n):
+    """Blocks up to the throughput encoder's 16 MiB limit and one byte past it
+    (the general encoder), byte-identical to the oracle, and decoded back."""
+    blk = _large_block(n, n)
+    comps, st = gu.gpu_compress(torch, [blk], dev)
+    assert st == [0]
+    assert comps[0] == oracle.compress(blk)
+    outs, st2, _ = gu.gpu_decompress(torch, comps, [n], dev)
+    assert st2 == [0] and outs[0] == blk
