@@ -316,3 +316,24 @@ def test_large_blocks_vs_oracle(dev, gu, oracle, n):
     assert comps[0] == oracle.compress(blk)
     outs, st2, _ = gu.gpu_decompress(torch, comps, [n], dev)
     assert st2 == [0] and outs[0] == blk
+
+
+def test_decode_full_grammar_streams(dev, gu, oracle):
+    """Valid LZO1X streams the LZO1X-1 compressor never writes (M1 after a
+    literal run and after trailing literals, long length extensions, M4
+    distances above 0x8000, 1-3 byte first runs): bit-exact on the GPU, and
+    the throughput decoder takes them all."""
+    import lzo_streams
+    streams = [lzo_streams.stream(1000 + s, [50, 300, 5000, 40000, 150000][s % 5])
+               for s in range(160)]
+    comps = [z for z, _ in streams]
+    want = [o for _, o in streams]
+    outs, st, fallbacks = gu.gpu_decompress_fast(torch, comps, [len(o) for o in want], dev)
+    assert st == [0] * len(want)
+    assert outs == want
+    assert fallbacks == 0
+    # the exact decoder on the same streams (capacity one byte short: OUTPUT_OVERRUN)
+    outs2, st2, _ = gu.gpu_decompress(torch, comps, [len(o) - 1 for o in want], dev)
+    for z, o, s, got in zip(comps, want, st2, outs2):
+        rc, ref = oracle.decompress_safe(z, len(o) - 1)
+        assert (s, got) == (rc, ref)

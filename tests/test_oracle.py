@@ -82,3 +82,13 @@ def test_oracle_vs_reference_fuzz(oracle, ref_lib):
                 z[rng.randrange(len(z))] = rng.getrandbits(8)
         cap = rng.randrange(0, n + 40)
         assert oracle.decompress_safe(bytes(z), cap) == ref_lib.decompress_safe(bytes(z), cap)
+
+
+def test_generated_full_grammar_streams(oracle, ref_lib):
+    """tests/lzo_streams.py (M1 forms, long extensions, far M4, short first
+    runs) decodes to its known output under the oracle and the reference."""
+    import lzo_streams
+    for seed in range(120):
+        z, out = lzo_streams.stream(seed, [50, 300, 5000, 40000][seed % 4])
+        assert oracle.decompress_safe(z, len(out)) == (0, out), seed
+        assert ref_lib.decompress_safe(z, len(out)) == (0, out), seed
