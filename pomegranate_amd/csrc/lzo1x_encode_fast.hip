@@ -58,8 +58,8 @@ constexpr uint32_t kTok = POM_ENC_TOK;          // token queue entries
 constexpr uint32_t kClaim = POM_ENC_CLAIM;      // claim table entries (slots hashed)
 constexpr uint32_t kStage = POM_ENC_STAGE;      // emitter output ring
 constexpr uint32_t kM2MaxOffset = 0x800;        // lib/minilzo.c M2_MAX_OFFSET
-constexpr uint32_t kNoLane = 0xFFFFFFFFu;
 constexpr uint32_t kM4MaxOffset = 0xBFFF;       // M4_MAX_OFFSET
+constexpr uint32_t kFarPos = 0xC0000000u;        // a read position past every block (kMaxN)
 #ifndef POM_EMIT_SLEEP
 #define POM_EMIT_SLEEP 8
 #endif
@@ -84,6 +84,18 @@ static_assert(sizeof(EncLds) * 4 <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ uint32_t lane_id() { return emit::lane(); }
 __device__ __forceinline__ uint32_t claim_index(uint32_t slot) { return (slot ^ (slot >> 9)) & (kClaim - 1); }
+
+// Inclusive prefix sum over the wave.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (uint32_t d = 1; d < (uint32_t)kWave; d <<= 1) {
+        const uint32_t u = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l - d) << 2), (int)v);
+        v += l >= d ? u : 0u;
+    }
+    return v;
+}
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ void wave_order() { emit::order(); }
@@ -142,8 +154,11 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 #ifndef POM_ENC_PATHMAX
 #define POM_ENC_PATHMAX 4                        // matches the path walk takes per window
 #endif
-#ifndef POM_ENC_DEFER
-#define POM_ENC_DEFER 0                          // extend a match leaving the window after the cut
+#ifndef POM_ENC_BATCH
+#define POM_ENC_BATCH 1                          // the emit wave writes up to 64 tokens per pass
+#endif
+#ifndef POM_ENC_FWD
+#define POM_ENC_FWD 8                            // claim conflicts resolved in place per window
 #endif
 constexpr int kCmpW = POM_ENC_CMP;
 constexpr uint32_t kCmpB = 4 * kCmpW;            // match bytes known without an extension
@@ -188,7 +203,7 @@ __device__ uint32_t extend_match(const BlockSrc& B, uint32_t n, uint32_t mc, uin
 // Diagnostic build only (STAMPS): per-phase s_memtime cycle sums and counts of
 // the parse wave go to stamps[b * kEncStampSlots + i]; no output depends on them.
 enum { EP_SETUP, EP_PROBE, EP_CAND, EP_PATH, EP_CLAIM, EP_TOK, EP_DICT, EP_PUSHWAIT,
-       EC_WINDOWS, EC_EXTEND, EC_TOKENS, EC_PATHIT, EC_EXTIT, EC_C2NEED, EC_C2MATCH, EP_N };
+       EC_WINDOWS, EC_EXTEND, EC_TOKENS, EC_PATHIT, EC_EXTIT, EC_C2NEED, EC_C2MATCH, EC_FWD, EP_N };
 constexpr int kEncStampSlots = 16;
 
 template <bool STAMPS>
@@ -281,16 +296,16 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             const uint32_t b3 = pw[0] >> 24;
             // (selects, no branches)
             const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
-            const bool use2 = v1 && !c1pass;         // the secondary slot is read and written
+            bool use2 = v1 && !c1pass;               // the secondary slot is read and written
             const bool c2pass = use2 && v2 && (p - w2 <= kM2MaxOffset || (c2w[0] >> 24) == b3);
             const bool tm = c1pass || c2pass;
-            const uint32_t slot = use2 ? h2 : h1, cand = c2pass ? w2 : w1;
+            uint32_t slot = use2 ? h2 : h1, cand = c2pass ? w2 : w1;
             uint32_t cw[kCmpW];
 #pragma unroll
             for (int i = 0; i < kCmpW; i++)
                 cw[i] = c2pass ? c2w[i] : c1w[i];
             // try_match (:2962-2971), then the match length as far as kCmpB bytes
-            const bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
+            bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
             uint32_t mlen = first_diff<kCmpW>(cw, pw);
             mlen = mlen < n - p ? mlen : n - p;
 
@@ -298,83 +313,112 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             // From lane 0: a matching lane jumps over its match, any other
             // lane is a literal.  Lanes inside matches neither probe nor
             // update the dictionary (:3051-3150).
-            const uint64_t okm = wave_ballot(ok);
+            uint64_t okm = wave_ballot(ok);
             if (STAMPS) {
                 __builtin_amdgcn_s_waitcnt(0);       // (attribute the candidate loads here)
-                const bool need2 = v1 && v2 && !(p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
-                acc[EC_C2NEED] += wave_ballot(need2) != 0;
-                acc[EC_C2MATCH] += wave_ballot(ok && slot == h2) != 0;
+                acc[EC_C2NEED] += wave_ballot(use2) != 0;
+                acc[EC_C2MATCH] += wave_ballot(ok && use2) != 0;
             }
             ESTAMP(EP_CAND);
             uint64_t path = 0, mstart = 0;
             uint32_t end = 0;                        // lane where the path leaves the window
-            uint32_t deferred = kNoLane;             // a match left unextended: it leaves the window anyway
             uint32_t nmatch = 0;
-            while (end < nact) {
-                if (STAMPS)
-                    acc[EC_PATHIT] += 1;
-                const uint64_t rest = okm & (~0ull << end);
-                const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
-                const uint32_t lit_end = q < nact ? q : nact;
-                if (lit_end > end)                   // literal lanes end .. lit_end-1
-                    path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
-                if (q >= nact) {
-                    end = nact;
-                    break;
-                }
-                path |= 1ull << q;
-                mstart |= 1ull << q;
-                uint32_t len = lane_read(mlen, q);
-                if (len == kCmpB && n - (ip + q) > kCmpB) {
-                    if (POM_ENC_DEFER && q + kCmpB >= nact) {   // its length only matters if kept
-                        deferred = q;
-                        end = q + kCmpB;
+            // the path from lane `from` on (lanes below it stay as they are)
+            auto walk = [&](uint32_t from) {
+                end = from;
+                while (end < nact) {
+                    if (STAMPS)
+                        acc[EC_PATHIT] += 1;
+                    const uint64_t rest = okm & (~0ull << end);
+                    const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
+                    const uint32_t lit_end = q < nact ? q : nact;
+                    if (lit_end > end)               // literal lanes end .. lit_end-1
+                        path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
+                    if (q >= nact) {
+                        end = nact;
                         break;
                     }
-                    if (STAMPS)
-                        acc[EC_EXTEND] += 1;
-                    len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
-                    if (STAMPS)
-                        acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
-                    mlen = l == q ? len : mlen;
+                    path |= 1ull << q;
+                    mstart |= 1ull << q;
+                    uint32_t len = lane_read(mlen, q);
+                    if (len == kCmpB && n - (ip + q) > kCmpB) {
+                        if (STAMPS)
+                            acc[EC_EXTEND] += 1;
+                        len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
+                        if (STAMPS)
+                            acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
+                        mlen = l == q ? len : mlen;
+                    }
+                    end = q + len;
+                    if (++nmatch >= POM_ENC_PATHMAX) // the window ends after this match
+                        break;
                 }
-                end = q + len;
-                if (++nmatch >= POM_ENC_PATHMAX)     // the window ends after this match
-                    break;
-            }
+            };
+            walk(0);
 
             ESTAMP(EP_PATH);
-            // ---- exactness: claims among the path lanes only ------------------
-            // Path lane l read h1 (and h2 when slot is h2) and writes slot.
-            // The table keeps, per hashed slot, the lowest lane of this window
+            // ---- exactness: claims among the path lanes, and forwarding ------
+            // Path lane l read h1 (and h2 when use2) and writes slot.  The
+            // table keeps, per hashed slot, the lowest lane of this window
             // writing it (ds_min of tag|lane; a wave's LDS operations complete
             // in order, so the reads below see every post).  A path lane is
-            // inexact only if a lower path lane writes a slot it read.
-            const bool onpath = (path >> l) & 1ull;
-            const uint32_t mine = (wtag << 8) | l;
-            atomicMin(&S.claim[onpath ? claim_index(slot) : kClaim], mine);
-            wave_order();
-            const uint32_t t1 = S.claim[claim_index(h1)];
-            const uint32_t t2 = S.claim[claim_index(h2)];
-            const bool conflicted = onpath && (((t1 >> 8) == wtag && (t1 & 0xFFu) < l) ||
-                                               (use2 && (t2 >> 8) == wtag && (t2 & 0xFFu) < l));
-            wtag--;
-            const uint64_t cm = wave_ballot(conflicted);
-            uint32_t cut = cm ? (uint32_t)__builtin_ctzll(cm) : 0xFFFFFFFFu;   // never lane 0
-#ifdef POM_ENC_MAXLANES
-            cut = cut < POM_ENC_MAXLANES ? cut : POM_ENC_MAXLANES;   // (debugging: a path lane)
-            while (cut < 64 && !((path >> cut) & 1ull))
-                cut++;
-#endif
-            if (cut < end)                           // the window ends at a path lane
-                end = cut;
-            if (deferred != kNoLane && deferred < end) {   // the unextended match is kept: its length
+            // inexact only if a lower path lane writes a slot it read.  The
+            // first such lane c is decided again: its entry is the position of
+            // the last lower path lane j writing that slot -- less than 64
+            // back, so the candidate passes the M2_MAX_OFFSET test -- and j's
+            // probe words are the candidate's bytes.  The path is walked again
+            // from c and the claims re-posted under a new tag; after
+            // POM_ENC_FWD such rounds the window ends at the next such lane.
+            uint64_t resolved = 0, superseded = 0;   // (superseded: a later lane writes its slot)
+            for (uint32_t round = 0;; round++) {
+                const bool onpath = (path >> l) & 1ull;
+                const uint32_t mine = (wtag << 8) | l;
+                atomicMin(&S.claim[onpath ? claim_index(slot) : kClaim], mine);
+                wave_order();
+                const uint32_t t1 = S.claim[claim_index(h1)];
+                const uint32_t t2 = S.claim[claim_index(h2)];
+                const bool cf1 = ((t1 >> 8) == wtag) & ((t1 & 0xFFu) < l);
+                const bool cf2 = use2 & ((t2 >> 8) == wtag) & ((t2 & 0xFFu) < l);
+                const bool fresh = ((resolved >> l) & 1ull) == 0;
+                const uint64_t cm = wave_ballot(onpath & fresh & (cf1 | cf2));
+                wtag--;
+                if (!cm)
+                    break;
+                const uint32_t c = (uint32_t)__builtin_ctzll(cm);   // never lane 0
+                if (round >= POM_ENC_FWD) {
+                    end = c;                         // the window ends at a path lane
+                    break;
+                }
                 if (STAMPS)
-                    acc[EC_EXTEND] += 1;
-                const uint32_t len = extend_match(B, n, lane_read(cand, deferred), ip + deferred,
-                                                  kCmpB, l);
-                mlen = l == deferred ? len : mlen;
-                end = deferred + len;
+                    acc[EC_FWD] += 1;
+                resolved |= 1ull << c;
+                const uint64_t below_c = (1ull << c) - 1;
+                const uint64_t pm = path & below_c;  // exact path lanes below c
+                const uint32_t h1c = lane_read(h1, c), h2c = lane_read(h2, c);
+                const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
+                const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (((wave_ballot(use2) >> c) & 1ull) ? ~0ull : 0ull);
+                if (!wm1 && !wm2)
+                    continue;                        // a claim-table alias: c was exact
+                const bool via2 = wm1 == 0;          // h1 unchanged, its test failed again: h2
+                const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
+                superseded |= 1ull << j;             // c writes j's slot after j
+                uint32_t pj[kCmpW];
+#pragma unroll
+                for (int i = 0; i < kCmpW; i++)
+                    pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)pw[i]);
+                uint32_t mc = first_diff<kCmpW>(pj, pw);
+                mc = mc < n - p ? mc : n - p;
+                const bool isc = l == c;
+                ok = isc ? ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0 : ok;
+                mlen = isc ? mc : mlen;
+                cand = isc ? ip + j : cand;
+                slot = isc ? (via2 ? h2 : h1) : slot;
+                use2 = isc ? via2 : use2;
+                okm = wave_ballot(ok);
+                path &= below_c;
+                mstart &= below_c;
+                nmatch = (uint32_t)__builtin_popcountll(mstart);
+                walk(c);
             }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
 
@@ -415,9 +459,9 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 const uint32_t last = 63 - (uint32_t)__builtin_clzll(km);
                 ii = ip + last + lane_read(mlen, last);
             }
-            // UPDATE_I of every path lane before the cut; their slots are distinct
+            // UPDATE_I of every path lane before the cut but the superseded ones: their slots are distinct
             ESTAMP(EP_TOK);
-            S.dict[(path & keep) >> l & 1ull ? slot : kSlots] = (uint16_t)(p - base + 1);
+            S.dict[(path & keep & ~superseded) >> l & 1ull ? slot : kSlots] = (uint16_t)(p - base + 1);
             wave_order();
             ESTAMP(EP_DICT);
             if (done)
@@ -475,6 +519,104 @@ __device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out
         if (x == 0x9E3779B9u)                        // (keeps the loads; never matters)
             S.sink = x;
     };
+    // Lane-parallel emission of the pending tokens, lane k writing token
+    // ct + k: the byte offsets are a prefix sum of the token sizes, a short
+    // literal run's length goes into the previous match's second-to-last
+    // byte (lib/minilzo.c:3027-3030: lane k-1's, or the staged byte before
+    // the batch), and the literal bytes of all lanes come in one load round
+    // trip.  The batch ends before the first token that is the tail, has more
+    // than kLitMax literals, needs extension zeros, fails the checks below,
+    // or would overrun the ring; that token takes the one-at-a-time path.
+    // Returns the number of tokens written.
+    constexpr uint32_t kLitMax = 16;
+    const BlockSrc B = block_src(in, n);
+    auto emit_batch = [&](uint32_t prod) -> uint32_t {
+        const uint32_t k = lane_id();
+        const uint32_t avail = prod - ct < (uint32_t)kWave ? prod - ct : (uint32_t)kWave;
+        const uint4 t = S.tok[(ct + (k < avail ? k : 0u)) % kTok];
+        const uint32_t r = t.y, L = t.z, d = t.w;
+        const uint32_t hdr = r >= 4 ? 1u : 0u;             // r <= kLitMax: one byte r - 3
+        const bool m2 = L <= 8 && d <= 0x800;
+        const bool near = d <= 0x4000;
+        const uint32_t lim = near ? 33u : 9u;               // longest length of the short form
+        const bool shortlen = L <= 8 || L <= lim;
+        const uint32_t msz = m2 ? 2u : shortlen ? 3u : 4u;
+        const uint32_t sz = hdr + r + msz;
+        const uint32_t adv = r + L;
+        const uint32_t iadv = wave_incl_sum(adv);
+        const uint32_t isz = wave_incl_sum(sz);
+        const uint32_t pk = pos + iadv - adv;              // input position of token k
+        const uint32_t budget = e.smask + 1 - (e.op - e.flushed) - 4;
+        const bool fits = k < avail && L != 0 && r <= kLitMax && (shortlen || L - lim <= 255) &&
+                          t.x == pk && r <= n - pk && L <= n - pk - r && d != 0 && d <= pk + r &&
+                          d <= kM4MaxOffset && isz <= budget;
+        const uint64_t bad = wave_ballot(!fits);
+        const uint32_t nb = bad ? (uint32_t)__builtin_ctzll(bad) : (uint32_t)kWave;
+        if (nb == 0)
+            return 0;
+        const bool act = k < nb;
+        const uint32_t m = e.smask;
+        uint8_t* const st = e.stage;
+        const uint32_t o = e.op + isz - sz;                // token k's first byte
+        const uint32_t rn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((k + 1) & 63u) << 2), (int)r);
+        const uint32_t pbits = k + 1 < nb && rn <= 3 ? rn : 0u;
+        if (k == 0 && r >= 1 && r <= 3)
+            st[(e.op - 2) & m] |= (uint8_t)r;
+        wave_order();
+        if (act && hdr)
+            st[o & m] = (uint8_t)(r - 3);
+        uint32_t lw[kLitMax / 4];
+        {
+            const uint32_t a = (act && r ? t.x : kFarPos) + B.sh0;
+            uint32_t raw[kLitMax / 4 + 1];
+#pragma unroll
+            for (uint32_t i = 0; i <= kLitMax / 4; i++)
+                raw[i] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, (a & ~3u) + 4 * i, 0, 0);
+#pragma unroll
+            for (uint32_t i = 0; i < kLitMax / 4; i++)
+                lw[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], a & 3u);
+        }
+        const uint32_t ol = o + hdr;
+#pragma unroll
+        for (uint32_t i = 0; i < kLitMax; i++)
+            if (act && i < r)
+                st[(ol + i) & m] = (uint8_t)(lw[i >> 2] >> (8 * (i & 3)));
+        // the match (lib/minilzo.c:3064-3145), the next run's length ORed in
+        const uint32_t oo = near ? d - 1 : d - 0x4000;
+        const uint32_t dlo = (oo & 63) << 2, dhi = oo >> 6;
+        const uint32_t tagb = near ? 0x20u : 0x10u | ((oo & 0x4000) >> 11);
+        uint32_t b0, b1, b2 = 0, b3 = 0;
+        if (m2) {
+            b0 = ((L - 1) << 5) | ((oo & 7) << 2);
+            b1 = oo >> 3;
+        } else if (shortlen) {
+            b0 = tagb | (L - 2);
+            b1 = dlo;
+            b2 = dhi;
+        } else {
+            b0 = tagb;
+            b1 = L - lim;                                  // ext(L - lim), no zero bytes
+            b2 = dlo;
+            b3 = dhi;
+        }
+        b0 |= msz == 2 ? pbits : 0u;
+        b1 |= msz == 3 ? pbits : 0u;
+        b2 |= msz == 4 ? pbits : 0u;
+        const uint32_t om = ol + r;
+        if (act) {
+            st[om & m] = (uint8_t)b0;
+            st[(om + 1) & m] = (uint8_t)b1;
+        }
+        if (act && msz >= 3)
+            st[(om + 2) & m] = (uint8_t)b2;
+        if (act && msz == 4)
+            st[(om + 3) & m] = (uint8_t)b3;
+        wave_order();
+        e.op += lane_read(isz, nb - 1);
+        pos += lane_read(iadv, nb - 1);
+        emit::maybe_flush(e);
+        return nb;
+    };
     for (;;) {
         prefetch();
         const uint32_t prod = lds_load(&S.prod);
@@ -483,6 +625,16 @@ __device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out
             continue;
         }
         while (ct < prod) {
+#ifndef POM_ENC_NOEMIT
+            if (POM_ENC_BATCH && !poisoned) {
+                const uint32_t nb = emit_batch(prod);
+                if (nb) {
+                    ct += nb;
+                    lds_store(&S.cons, ct);
+                    continue;
+                }
+            }
+#endif
             const uint4 t = S.tok[ct % kTok];
             ct++;
             // Every token must continue where the last one ended and stay in
