@@ -152,7 +152,7 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 #define POM_ENC_CMP 8                            // dwords compared in the window round trip
 #endif
 #ifndef POM_ENC_PATHMAX
-#define POM_ENC_PATHMAX 4                        // matches the path walk takes per window
+#define POM_ENC_PATHMAX 6                        // matches the path walk takes per window
 #endif
 #ifndef POM_ENC_BATCH
 #define POM_ENC_BATCH 1                          // the emit wave writes up to 64 tokens per pass
