@@ -72,7 +72,9 @@ int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len,
 int lzo_mi355x_compress_batch(const uint8_t *const *src, const size_t *src_len,
                               uint8_t *const *dst, size_t *dst_len, int *status,
                               size_t nblocks);
-/* dst_len[b] is the capacity in and the produced length out. */
+/* dst_len[b] is the capacity in and the produced length out.  Both batch
+ * calls stage every input before they write any output, so dst[b] may overlap
+ * src[b] (in-place decoding). */
 int lzo_mi355x_decompress_batch(const uint8_t *const *src, const size_t *src_len,
                                 uint8_t *const *dst, size_t *dst_len, int *status,
                                 size_t nblocks);

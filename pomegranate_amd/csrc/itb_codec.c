@@ -5,8 +5,8 @@
  * The per-record semantics follow the reference one for one:
  *   compress   mds/itb.c:2904-2945  (header copy, incompressible fallback,
  *                                    len/zlen swap, COMPR_LZO)
- *   decompress mds/itb.c:2949-2980, mdsl/gc.c:755-786 (payload copied aside,
- *                                    decoded in place, COMPR_NONE, len back)
+ *   decompress mds/itb.c:2949-2980, mdsl/gc.c:755-786 (decoded in place,
+ *                                    COMPR_NONE, len back)
  *   append     mdsl/storage.c:455-519 (append_buf_write), :384-451
  *              (append_buf_flush_remap)
  * The LZO work of a whole batch is one GPU round trip (lzo_host.c).
@@ -104,26 +104,18 @@ int pom_itb_lzo_decompress_batch(uint8_t *const *in, const size_t *cap, int *err
     uint8_t **dst = malloc(n * sizeof(*dst));
     size_t *slen = malloc(n * sizeof(*slen));
     size_t *dlen = malloc(n * sizeof(*dlen));
-    size_t *off = malloc(n * sizeof(*off));
     int *st = malloc(n * sizeof(*st));
-    uint8_t *copy = NULL;
     int rc = LZO_E_OUT_OF_MEMORY;
-    if (!src || !dst || !slen || !dlen || !off || !st)
+    if (!src || !dst || !slen || !dlen || !st)
         goto out;
-    size_t total = 0;
     for (size_t b = 0; b < n; b++) {
         const uint32_t len = rd32(in[b] + POM_ITBH_LEN_OFF);
         slen[b] = len >= POM_ITBH_SIZE ? len - POM_ITBH_SIZE : 0;
-        off[b] = total;
-        total += slen[b];
     }
-    /* the payloads are copied aside: the output overwrites them in place */
-    copy = malloc(total ? total : 1);
-    if (!copy)
-        goto out;
+    /* in place: the batch call stages every payload before it writes any
+     * output (include/lzo_mi355x.h), so no copy aside is needed */
     for (size_t b = 0; b < n; b++) {
-        memcpy(copy + off[b], in[b] + POM_ITBH_SIZE, slen[b]);
-        src[b] = copy + off[b];
+        src[b] = in[b] + POM_ITBH_SIZE;
         dst[b] = in[b] + POM_ITBH_SIZE;
         dlen[b] = cap[b] > POM_ITBH_SIZE ? cap[b] - POM_ITBH_SIZE : 0;
     }
@@ -139,12 +131,10 @@ int pom_itb_lzo_decompress_batch(uint8_t *const *in, const size_t *cap, int *err
         wr32(in[b] + POM_ITBH_LEN_OFF, (uint32_t)(dlen[b] + POM_ITBH_SIZE));
     }
 out:
-    free(copy);
     free(src);
     free(dst);
     free(slen);
     free(dlen);
-    free(off);
     free(st);
     return rc;
 }

@@ -268,6 +268,24 @@ static void copy_jobs(const struct copy_job *jobs, size_t n)
             pthread_join(th[j], NULL);
 }
 
+void pom_copy_parallel(uint8_t *const *dst, const uint8_t *const *src, const size_t *len, size_t n)
+{
+    struct copy_job *jobs = malloc(n * sizeof(*jobs));
+    if (!jobs) {
+        for (size_t i = 0; i < n; i++)
+            if (len[i])
+                memcpy(dst[i], src[i], len[i]);
+        return;
+    }
+    for (size_t i = 0; i < n; i++) {
+        jobs[i].dst = dst[i];
+        jobs[i].src = src[i];
+        jobs[i].len = len[i];
+    }
+    copy_jobs(jobs, n);
+    free(jobs);
+}
+
 /* Staging layout (identical on host and device, so one copy each way):
  *   [src_off u64][dst_off u64][src_len u32][dst_cap u32][out_len u32][status i32]
  *   [packed offset u64]

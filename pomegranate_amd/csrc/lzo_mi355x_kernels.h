@@ -56,6 +56,10 @@ int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off
                                      const uint32_t *src_len, uint32_t *out_len,
                                      int32_t *status, uint32_t nblocks, hipStream_t stream);
 
+/* Host side (lzo_host.c), not part of the ABI: len[i] bytes from src[i] to
+ * dst[i] for every i, split over up to 8 threads once the total is large. */
+void pom_copy_parallel(uint8_t *const *dst, const uint8_t *const *src, const size_t *len, size_t n);
+
 /* Block b's first min(len[b], cap[b]) bytes at from + from_off[b] go to
  * to + to_off[b] (offsets 16-byte aligned, regions padded to 16 bytes). */
 int lzo_mi355x_launch_pack(const uint8_t *from, const uint64_t *from_off, const uint32_t *len,

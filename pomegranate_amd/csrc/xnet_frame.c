@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "lzo_mi355x_kernels.h"
 #include "minilzo.h"
 #include "pom_itb.h"
 #include "pom_xnet.h"
@@ -146,22 +147,24 @@ int pom_xnet_itb_recv_batch(const struct pom_xnet_frame *f, size_t n, uint8_t *c
     size_t *cap = malloc(n * sizeof(*cap));
     size_t *at = malloc(n * sizeof(*at));
     int *derr = malloc(n * sizeof(*derr));
+    const uint8_t **csrc = malloc(n * sizeof(*csrc));
+    size_t *clen = malloc(n * sizeof(*clen));
     int rc = LZO_E_OUT_OF_MEMORY;
-    if (!dec || !cap || !at || !derr)
+    if (!dec || !cap || !at || !derr || !csrc || !clen)
         goto out;
+    /* the data of every frame into its ITB buffer (threaded copies) */
+    for (size_t b = 0; b < n; b++) {
+        const uint32_t len = f[b].tx.len;
+        err[b] = f[b].dropped ? -EBADMSG : len < POM_ITBH_SIZE || len > itb_cap ? -EIO : 0;
+        csrc[b] = f[b].data;
+        clen[b] = err[b] ? 0 : len;
+    }
+    pom_copy_parallel(itb, csrc, clen, n);
     size_t nd = 0;
     for (size_t b = 0; b < n; b++) {
-        err[b] = 0;
-        if (f[b].dropped) {
-            err[b] = -EBADMSG;
+        if (err[b])
             continue;
-        }
         const uint32_t len = f[b].tx.len;
-        if (len < POM_ITBH_SIZE || len > itb_cap) {
-            err[b] = -EIO;
-            continue;
-        }
-        memcpy(itb[b], f[b].data, len);
         if (rd32(itb[b] + POM_ITBH_LEN_OFF) != len) {   /* the load path's ASSERT */
             err[b] = -EIO;
             continue;
@@ -184,5 +187,7 @@ out:
     free(cap);
     free(at);
     free(derr);
+    free(csrc);
+    free(clen);
     return rc;
 }
