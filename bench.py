@@ -412,7 +412,7 @@ def run_c5(args, rank):
             which, err = itb.compress_batch(recs, tmps)         # H2D + kernels + D2H
             t1 = time.perf_counter()
             af = itb.AppendFile(path)
-            locs = [af.append(o[: itb.header_fields(o)[0]])
+            locs = [af.append(o, itb.header_fields(o)[0])
                     for o in (t if w else r for r, t, w in zip(recs, tmps, which))]
             af.close()
             t2 = time.perf_counter()

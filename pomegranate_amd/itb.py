@@ -127,10 +127,18 @@ class AppendFile:
         if rc:
             raise OSError(-rc, os.strerror(-rc), path)
 
-    def append(self, rec) -> int:
+    def append(self, rec, length: "int | None" = None) -> int:
+        """Appends the first `length` bytes (default all) of rec: bytes, or a
+        writable buffer (bytearray, memoryview) passed without a copy."""
         loc = ctypes.c_uint64(0)
-        buf = bytes(rec)
-        rc = self.lib.pom_abuf_append(ctypes.byref(self.ab), buf, len(buf), ctypes.byref(loc))
+        n = len(rec) if length is None else length
+        if isinstance(rec, bytes):
+            ptr, keep = rec, None
+        else:
+            keep = (ctypes.c_char * len(rec)).from_buffer(rec)
+            ptr = ctypes.addressof(keep)
+        rc = self.lib.pom_abuf_append(ctypes.byref(self.ab), ptr, n, ctypes.byref(loc))
+        del keep
         if rc:
             raise OSError(-rc, os.strerror(-rc))
         return loc.value
