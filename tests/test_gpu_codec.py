@@ -337,3 +337,47 @@ def test_decode_full_grammar_streams(dev, gu, oracle):
     for z, o, s, got in zip(comps, want, st2, outs2):
         rc, ref = oracle.decompress_safe(z, len(o) - 1)
         assert (s, got) == (rc, ref)
+
+
+def _sweep_blocks(count, seed):
+    """Random sizes (0..300 KB) over every content model, with transforms that
+    make dense in-window repeats: short periodic stretches, copied runs at
+    distances 1..70 (claim conflicts and in-window forwarding), and byte
+    noise."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        n = int(rng.integers(0, 300000)) if i % 4 else int(rng.integers(0, 2000))
+        d = bytearray(synth.block(int(rng.integers(0, 6)), int(rng.integers(0, 1 << 30)), n))
+        for _ in range(int(rng.integers(0, 8))):
+            if n < 200:
+                break
+            a = int(rng.integers(0, n - 100))
+            L = int(rng.integers(4, min(4000, n - a)))
+            k = int(rng.integers(0, 3))
+            if k == 0:                                  # periodic stretch
+                per = int(rng.integers(1, 70))
+                for j in range(a + per, a + L):
+                    d[j] = d[j - per]
+            elif k == 1:                                # a copied run close behind
+                dist = int(rng.integers(1, 71))
+                if a >= dist:
+                    for j in range(a, a + L):
+                        d[j] = d[j - dist]
+            else:                                       # noise
+                for j in rng.integers(a, a + L, 16):
+                    d[int(j)] = int(rng.integers(0, 256))
+        out.append(bytes(d))
+    return out
+
+
+def test_encoder_random_sweep_vs_oracle(dev, gu, oracle):
+    """600 blocks across every content model and transform, byte-identical to
+    the oracle, then decoded back."""
+    blocks = _sweep_blocks(600, 77)
+    comps, st = gu.gpu_compress(torch, blocks, dev, shift=2)
+    assert all(s == 0 for s in st)
+    bad = [i for i, (b, c) in enumerate(zip(blocks, comps)) if c != oracle.compress(b)]
+    assert not bad, bad[:10]
+    outs, st2, _ = gu.gpu_decompress(torch, comps, [len(b) for b in blocks], dev, shift=1)
+    assert all(s == 0 for s in st2) and outs == blocks
