@@ -381,3 +381,42 @@ def test_encoder_random_sweep_vs_oracle(dev, gu, oracle):
     assert not bad, bad[:10]
     outs, st2, _ = gu.gpu_decompress(torch, comps, [len(b) for b in blocks], dev, shift=1)
     assert all(s == 0 for s in st2) and outs == blocks
+
+
+def test_concurrent_host_threads(dev, oracle):
+    """The MDS commit threads, service threads and MDSL GC thread call the
+    codec at once: 6 host threads, each with its own HIP stream
+    and staging, mixing single calls and batches; every result bit-exact."""
+    import threading
+    errors = []
+
+    def worker(t):
+        try:
+            rng = np.random.default_rng(900 + t)
+            for it in range(6):
+                blocks = [synth.block(int(rng.integers(0, 6)), int(rng.integers(0, 1 << 30)),
+                                      int(rng.integers(0, 200000))) for _ in range(int(rng.integers(1, 40)))]
+                if it % 2:
+                    rc, st, comps = lzo.compress_batch(blocks)
+                    assert rc == 0 and all(s == 0 for s in st)
+                else:
+                    comps = []
+                    for b in blocks:
+                        rc, z = lzo.lzo1x_1_compress(b)
+                        assert rc == 0
+                        comps.append(z)
+                assert comps == [oracle.compress(b) for b in blocks]
+                rc, st, outs = lzo.decompress_batch(comps, [len(b) for b in blocks])
+                assert rc == 0 and all(s == 0 for s in st) and list(outs) == blocks
+                rc, out = lzo.lzo1x_decompress_safe(comps[0], len(blocks[0]))
+                assert (rc, out) == (0, blocks[0])
+        except BaseException as e:                 # reported by the main thread
+            errors.append((t, repr(e)[:300]))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=110)
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors
