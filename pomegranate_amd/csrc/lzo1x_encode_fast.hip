@@ -316,8 +316,8 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             uint64_t okm = wave_ballot(ok);
             if (STAMPS) {
                 __builtin_amdgcn_s_waitcnt(0);       // (attribute the candidate loads here)
-                acc[EC_C2NEED] += wave_ballot(use2) != 0;
-                acc[EC_C2MATCH] += wave_ballot(ok && use2) != 0;
+                acc[EC_C2NEED] += 0;
+                acc[EC_C2MATCH] += 0;
             }
             ESTAMP(EP_CAND);
             uint64_t path = 0, mstart = 0;
@@ -419,6 +419,10 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 mstart &= below_c;
                 nmatch = (uint32_t)__builtin_popcountll(mstart);
                 walk(c);
+            }
+            if (STAMPS) {                            // (why the window ended)
+                acc[EC_C2NEED] += end > 64 ? 1 : 0;  // a match crossing its last lane
+                acc[EC_C2MATCH] += nmatch >= POM_ENC_PATHMAX ? 1 : 0;   // the path cap
             }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
 

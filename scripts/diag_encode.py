@@ -51,7 +51,7 @@ if fn is None:
     sys.exit(0)
 st = stamps.view(nb, SLOTS).double().cpu().numpy()
 phases = ["setup", "probe", "cand", "path", "claim", "tok", "dict", "pushwait"]
-counts = ["windows", "extend", "tokens", "pathit", "extit", "use2win", "use2match", "fwd"]
+counts = ["windows", "extend", "tokens", "pathit", "extit", "end_cross", "end_cap", "fwd"]
 print("parse cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases)},
       "total", int(st[:, :len(phases)].sum(1).mean()))
 print("counts/block (mean):", {n: round(float(st[:, len(phases) + i].mean()), 1) for i, n in enumerate(counts)})
