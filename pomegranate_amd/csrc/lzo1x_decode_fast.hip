@@ -75,6 +75,9 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_RING
 #define POM_RING 4096
 #endif
+#ifndef POM_WIDE
+#define POM_WIDE 1                               // 16-byte steps for batches of contiguous / period-1 ops
+#endif
 #ifndef POM_DUTY_EVERY
 #define POM_DUTY_EVERY 4                         // parser pass-1 iterations between writer duties
 #endif
@@ -406,6 +409,48 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
 }
 
+// Misaligned LDS accesses for the 16-byte steps.  gfx950 runs LDS in
+// unaligned mode: ds_read_b128 / ds_write_b128 / b64 / b32 / b16 at any byte
+// address are exact (scripts/probe/lds_misaligned_probe.hip; ~1.5x the
+// latency of an aligned access).  The compiler assumes natural alignment for
+// its own accesses, so these are written out.  The read waits for its data
+// itself; LDS accesses of one wave complete in order, so the compiler's own
+// lgkmcnt waits stay correct (they only become more conservative).
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t lds_off(const void* p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint4 lds_read16(uint32_t a)
+{
+    v4u32 v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_write16(uint32_t a, uint4 v)
+{
+    const v4u32 t = {v.x, v.y, v.z, v.w};
+    asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(t) : "memory");
+}
+__device__ __forceinline__ void lds_write8(uint32_t a, uint32_t lo, uint32_t hi)
+{
+    const v2u32 t = {lo, hi};
+    asm volatile("ds_write_b64 %0, %1" : : "v"(a), "v"(t) : "memory");
+}
+__device__ __forceinline__ void lds_write4(uint32_t a, uint32_t v)
+{
+    asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_write2(uint32_t a, uint32_t v)
+{
+    asm volatile("ds_write_b16 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_write1(uint32_t a, uint32_t v)
+{
+    asm volatile("ds_write_b8 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+
 
 
 // 4 bytes at an arbitrary global address via two aligned dword loads (an
@@ -491,7 +536,7 @@ enum { PH_STAGE, PH_PASS1, PH_PWALK, PH_MERGE, PH_COUNT, PH_WRITE, PH_PSLOT, PH_
        CN_FIRST, CN_WALKS = CN_FIRST, CN_IT_PASS1, CN_IT_PWALK, CN_IT_WALK, CN_IT_COUNT,
        CN_IT_WRITE, CN_PIECES,
        CN_WINDOWS, CN_SRCWIN, CN_SRCMISS, CN_BATCHES, CN_STEPS, CN_FWD_ROUNDS,
-       CN_REASON, PH_N };
+       CN_WBATCHES, CN_NW_GOP, CN_NW_PER, CN_REASON, PH_N };
 constexpr int kStampSlots = 40;
 static_assert(PH_N <= kStampSlots, "stamp slots per block");
 __device__ __forceinline__ bool parser_slot(int i)
@@ -1221,6 +1266,11 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             const uint32_t wchunks = lane_read(cinc, kWave - 1);
             S.wop[l] = make_uint4(o, db, cs, L | (gop ? kLitFlag : 0u));
             S.wper[l] = make_uint2(dp, inv);
+            // 16-byte steps take a batch whose ops all read a contiguous
+            // source (no self-overlap) or repeat one byte (period 1), none of
+            // it from HBM.  The ring rule of `gop` covers them: it bounds a
+            // source by the op's start and end, not by the step length.
+            const bool wide_ok = !gop && dp <= 1u;
             wave_order();
             STAMP(PH_FARC);
             uint32_t s = 0;
@@ -1236,6 +1286,130 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 STAMP(PH_BATCH);
                 if (STAMPS)
                     acc[CN_BATCHES] += 1;
+                if (STAMPS) {
+                    const bool wb = !wave_ballot(starter && !wide_ok);
+                    acc[CN_WBATCHES] += wb;
+                    acc[CN_NW_GOP] += !wb && wave_ballot(starter && gop);
+                    acc[CN_NW_PER] += !wb && !wave_ballot(starter && gop);
+                }
+                if (POM_WIDE && !wave_ballot(starter && !wide_ok)) {
+                    // ---- batch [s, e) in 16-byte chunks, 64 per step (1 KiB) --
+                    // Same chunk -> op mapping as below; each op's first
+                    // 16-byte chunk replaces its 4-byte one in wop.z (an op
+                    // belongs to one batch only).
+                    const uint32_t n16 = starter ? (L + 15u) >> 4 : 0u;
+                    const uint32_t inc16 = wave_incl_scan(n16);
+                    const uint32_t cs16 = inc16 - n16;
+                    const uint32_t end16 = lane_read(inc16, kWave - 1);
+                    if (starter)
+                        S.wop[l].z = cs16;
+                    const uint32_t base = lds_off(&S);
+                    uint32_t jc = s;
+                    for (uint32_t C = 0; C < end16; C += kWave) {
+                        tag++;
+                        const uint32_t tagv = tag | 0x80000000u;
+                        if (starter && cs16 >= C && cs16 < C + kWave)
+                            S.flags[cs16 - C] = tagv;
+                        wave_order();
+                        const bool st0 = S.flags[l] == tagv;
+                        const uint64_t M = wave_ballot(st0);
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+                        const uint32_t j = (jc + below + (st0 ? 0u : ~0u)) & 63u;
+                        jc += (uint32_t)__builtin_popcountll(M);
+                        const uint4 op = S.wop[j];
+                        const uint32_t p1 = S.wper[j].x;          // 0 or 1
+                        const uint32_t c = C + l;
+                        const bool live = c < end16;
+                        const uint32_t k16 = (c - op.z) * 16u;
+                        const uint32_t x = op.x + k16;
+                        const uint32_t rem = op.w - k16;          // (no kLitFlag: !gop)
+                        const uint32_t len = live ? (rem < 16u ? rem : 16u) : 0u;
+                        const uint32_t nl = end16 - C < (uint32_t)kWave ? end16 - C : (uint32_t)kWave;
+                        const uint32_t xs = lane_read(x, 0);
+                        const uint32_t step_end = lane_read(x + len, nl - 1);
+                        for (uint32_t spin = 0; step_end > issued_seen + kRing; spin++) {
+                            if (spin > (1u << 22)) {
+                                refuse = true;
+                                reason = RS_SPACE;
+                                break;
+                            }
+                            if (spin)
+                                __builtin_amdgcn_s_sleep(1);
+                            issued_seen = lds_load(&S.issued);
+                        }
+                        if (refuse)
+                            break;
+                        if (STAMPS)
+                            acc[CN_STEPS] += 1;
+                        (void)xs;
+                        // source: 16 contiguous bytes, or the one repeated byte
+                        const bool lin = (op.y & kLitFlag) != 0;
+                        const uint32_t sa = (op.y & ~kLitFlag) + (p1 ? 0u : k16);
+                        const uint32_t ra = !live ? 0u : lin ? (sa & kLdsMask) : (sa & kRingMask);
+                        const uint32_t need = p1 ? 1u : len;
+                        const bool rcross = live && !lin && ra + need > kRing;
+                        uint4 v = lds_read16(base + ra);
+                        if (wave_ballot(rcross)) {
+                            if (rcross) {                      // source wraps the ring end
+                                const uint8_t* lds = (const uint8_t*)&S;
+                                uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+                                for (uint32_t i = 0; i < 16; i++)
+                                    w[i >> 2] |= (uint32_t)lds[(sa + i) & kRingMask] << (8 * (i & 3));
+                                v = make_uint4(w[0], w[1], w[2], w[3]);
+                            }
+                        }
+                        if (p1) {
+                            const uint32_t b4 = (v.x & 0xFFu) * 0x01010101u;
+                            v = make_uint4(b4, b4, b4, b4);
+                        }
+                        // destination: the ring at x
+                        const uint32_t xd = x & kRingMask;
+                        const bool wcross = live && xd + len > kRing;
+                        if (live && !wcross) {
+                            const uint32_t da = base + xd;
+                            if (len == 16u) {
+                                lds_write16(da, v);
+                            } else {
+                                uint32_t w0 = v.x, w1 = v.y, ad = da;
+                                if (len & 8u) {
+                                    lds_write8(ad, v.x, v.y);
+                                    w0 = v.z;
+                                    w1 = v.w;
+                                    ad += 8;
+                                }
+                                if (len & 4u) {
+                                    lds_write4(ad, w0);
+                                    w0 = w1;
+                                    ad += 4;
+                                }
+                                if (len & 2u) {
+                                    lds_write2(ad, w0);
+                                    w0 >>= 16;
+                                    ad += 2;
+                                }
+                                if (len & 1u)
+                                    lds_write1(ad, w0);
+                            }
+                        }
+                        if (wave_ballot(wcross)) {
+                            if (wcross) {                      // destination wraps the ring end
+                                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                                for (uint32_t i = 0; i < 16; i++)
+                                    if (i < len)
+                                        lds_write1(base + ((x + i) & kRingMask), w[i >> 2] >> (8 * (i & 3)));
+                            }
+                        }
+                        wave_order();
+                        lds_store(&S.produced, step_end);
+                    }
+                    if (refuse)
+                        break;
+                    s = e;
+                    continue;
+                }
                 // ---- batch [s, e): chunks [c_beg, c_end), 64 per step --------
                 uint32_t jcarry = s;                   // ops of the batch started before C
                 for (uint32_t C = c_beg; C < c_end; C += kWave) {

@@ -65,7 +65,8 @@ phases = ["stage", "pass1", "pwalk", "merge", "count", "write", "p_slotwait", "p
           "e_wait", "wload", "wscan", "src_issue", "fwd", "src_commit+wop", "batch",
           "space", "flags", "gather", "publish"]
 counts = ["walks", "it_pass1", "it_pwalk", "it_walk", "it_count", "it_write", "pieces",
-          "windows", "src_windows", "src_miss", "batches", "steps", "fwd_rounds", "reason"]
+          "windows", "src_windows", "src_miss", "batches", "steps", "fwd_rounds", "wide_batches", "narrow_gop",
+          "narrow_period", "reason"]
 PARSER = 8   # phases [0, 8) belong to the parser wave, the rest to the executor
 ptot = st[:, :PARSER].sum(1); etot = st[:, PARSER:len(phases)].sum(1)
 print("parser cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases[:PARSER])},
