@@ -400,7 +400,7 @@ def _c5_xnet(args, recs, originals, tmps, rbufs, path, itb, xnet, plain_bytes):
         rc, wl, err = xnet.wb_batch(recs, tmps, dests, 0x11, 1, 3, wire)
         frames, used = xnet.parse(wire, wl, magic=3)
         af = itb.AppendFile(path)
-        locs = [af.append(memoryview(wire)[f.offset: f.offset + f.tx.len]) for f in frames]
+        locs = af.append_batch([memoryview(wire)[f.offset: f.offset + f.tx.len] for f in frames])
         af.close()
         t1 = time.perf_counter()
         fd = os.open(path, os.O_RDONLY)
@@ -451,8 +451,8 @@ def run_c5(args, rank):
             which, err = itb.compress_batch(recs, tmps)         # H2D + kernels + D2H
             t1 = time.perf_counter()
             af = itb.AppendFile(path)
-            locs = [af.append(o, itb.header_fields(o)[0])
-                    for o in (t if w else r for r, t, w in zip(recs, tmps, which))]
+            outs = [t if w else r for r, t, w in zip(recs, tmps, which)]
+            locs = af.append_batch(outs, [itb.header_fields(o)[0] for o in outs])
             af.close()
             t2 = time.perf_counter()
             fd = os.open(path, os.O_RDONLY)

@@ -73,6 +73,11 @@ struct pom_abuf {
 };
 int pom_abuf_open(struct pom_abuf *ab, const char *path, size_t win);
 int pom_abuf_append(struct pom_abuf *ab, const void *rec, size_t len, uint64_t *location);
+/* n appends in one call: the same file bytes and locations as n calls of
+ * pom_abuf_append in order (each window's share pre-faulted, copied by host
+ * threads).  recs[b] may be NULL only when lens[b] == 0. */
+int pom_abuf_append_batch(struct pom_abuf *ab, const void *const *recs, const size_t *lens,
+                          size_t n, uint64_t *locations);
 /* unmaps and trims the file to the appended length */
 int pom_abuf_close(struct pom_abuf *ab);
 

@@ -22,6 +22,7 @@
 #include "lzo_mi355x.h"
 #include "minilzo.h"
 #include "pom_itb.h"
+#include "lzo_mi355x_kernels.h"
 
 static uint32_t rd32(const uint8_t *p)
 {
@@ -207,6 +208,83 @@ int pom_abuf_append(struct pom_abuf *ab, const void *rec, size_t len, uint64_t *
     }
     ab->acclen += len;
     return 0;
+}
+
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+
+/* A batch of appends with the locations of n single appends in order.  Each
+ * window's share is pre-faulted in one madvise (page-by-page write faults on
+ * the shared mapping were the append's main cost) and copied by the threaded
+ * copier; a full window is unmapped and the next mapped as in
+ * pom_abuf_append. */
+int pom_abuf_append_batch(struct pom_abuf *ab, const void *const *recs, const size_t *lens,
+                          size_t n, uint64_t *locations)
+{
+    if (!ab->addr)
+        return -EINVAL;
+    uint8_t **dst = malloc((n + 1) * sizeof(*dst));
+    const uint8_t **src = malloc((n + 1) * sizeof(*src));
+    size_t *len = malloc((n + 1) * sizeof(*len));
+    if (!dst || !src || !len) {
+        free(dst);
+        free(src);
+        free(len);
+        return -ENOMEM;
+    }
+    const size_t page = (size_t)sysconf(_SC_PAGESIZE);
+    int rc = 0;
+    size_t b = 0, done = 0;         /* record b, bytes of it already placed */
+    while (b < n && !rc) {
+        /* jobs of the current window: from ab->offset up to its end */
+        size_t nj = 0, start = ab->offset, off = ab->offset;
+        while (b < n && off < ab->win) {
+            if (!recs[b] && lens[b]) {
+                rc = -EINVAL;
+                break;
+            }
+            if (done == 0 && locations)
+                locations[b] = ab->file_offset + off;
+            size_t w = ab->win - off;
+            if (w > lens[b] - done)
+                w = lens[b] - done;
+            if (w) {
+                dst[nj] = ab->addr + off;
+                src[nj] = (const uint8_t *)recs[b] + done;
+                len[nj] = w;
+                nj++;
+            }
+            off += w;
+            done += w;
+            if (done == lens[b]) {
+                ab->acclen += lens[b];
+                b++;
+                done = 0;
+            }
+        }
+        if (rc)
+            break;
+        if (off > start) {
+            const size_t p0 = start / page * page;
+            (void)madvise(ab->addr + p0, off - p0, MADV_POPULATE_WRITE);   /* best effort */
+            pom_copy_parallel(dst, src, len, nj);
+        }
+        ab->offset = off;
+        if (ab->offset >= ab->win) {
+            if (munmap(ab->addr, ab->win) != 0) {
+                rc = -errno;
+                break;
+            }
+            ab->addr = NULL;
+            ab->file_offset += ab->win;
+            rc = abuf_map(ab);
+        }
+    }
+    free(dst);
+    free(src);
+    free(len);
+    return rc;
 }
 
 int pom_abuf_close(struct pom_abuf *ab)

@@ -46,6 +46,8 @@ def _lib() -> ctypes.CDLL:
         lib.pom_abuf_append.restype = ctypes.c_int
         lib.pom_abuf_append.argtypes = [ctypes.POINTER(_Abuf), _vp, ctypes.c_size_t,
                                         ctypes.POINTER(ctypes.c_uint64)]
+        lib.pom_abuf_append_batch.restype = ctypes.c_int
+        lib.pom_abuf_append_batch.argtypes = [ctypes.POINTER(_Abuf), _vp, _vp, ctypes.c_size_t, _vp]
         lib.pom_abuf_close.restype = ctypes.c_int
         lib.pom_abuf_close.argtypes = [ctypes.POINTER(_Abuf)]
         lib.pom_itb_read.restype = ctypes.c_int
@@ -142,6 +144,32 @@ class AppendFile:
         if rc:
             raise OSError(-rc, os.strerror(-rc))
         return loc.value
+
+    def append_batch(self, recs, lengths=None) -> list:
+        """Appends the first lengths[i] bytes (default all) of each record in
+        one call (pom_abuf_append_batch): the file and the locations equal
+        those of append() called in order."""
+        n = len(recs)
+        ptrs = (ctypes.c_void_p * max(n, 1))()
+        lens = (ctypes.c_size_t * max(n, 1))()
+        locs = (ctypes.c_uint64 * max(n, 1))()
+        keep = []
+        for i, r in enumerate(recs):
+            if isinstance(r, bytes):
+                ptrs[i] = ctypes.cast(ctypes.c_char_p(r), ctypes.c_void_p).value
+                keep.append(r)
+            else:
+                c = (ctypes.c_char * len(r)).from_buffer(r)
+                keep.append(c)
+                ptrs[i] = ctypes.addressof(c)
+            lens[i] = len(r) if lengths is None else int(lengths[i])
+            if lens[i] > len(r):
+                raise ValueError(f"record {i}: length {lens[i]} > buffer {len(r)}")
+        rc = self.lib.pom_abuf_append_batch(ctypes.byref(self.ab), ptrs, lens, n, locs)
+        del keep
+        if rc:
+            raise OSError(-rc, os.strerror(-rc))
+        return list(locs[:n])
 
     def close(self) -> None:
         rc = self.lib.pom_abuf_close(ctypes.byref(self.ab))

@@ -47,7 +47,7 @@ EXPORTS = (
     "lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
     # include/pom_itb.h
     "pom_itb_lzo_compress_batch", "pom_itb_lzo_decompress_batch",
-    "pom_abuf_open", "pom_abuf_append", "pom_abuf_close", "pom_itb_read",
+    "pom_abuf_open", "pom_abuf_append", "pom_abuf_append_batch", "pom_abuf_close", "pom_itb_read",
     # include/pom_column.h
     "pom_col_zip_bound", "pom_col_zip_batch", "pom_col_zipv", "pom_col_unzip_batch",
     # include/pom_xnet.h
@@ -72,6 +72,14 @@ def load() -> ctypes.CDLL:
         raise RuntimeError(
             f"{LIB_PATH} is missing: run __graft_entry__.build(); the LZO1X "
             "path has no CPU fallback")
+    # torch bundles its own HIP runtime.  Loading it first lets this library
+    # bind to that same libamdhip64 (by soname); loaded the other way round the
+    # process holds two HIP runtimes, and the one initialised second sees no
+    # GPU (hipGetDeviceCount = 0 on the GPU box).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     lib.__lzo_init_v2.restype = ctypes.c_int
     lib.__lzo_init_v2.argtypes = [ctypes.c_uint] + [ctypes.c_int] * 9

@@ -48,6 +48,31 @@ def test_append_file_round_trip(tmp_path):
         os.close(fd)
 
 
+@pytest.mark.parametrize("win", [1 << 20, 4096 * 3, 64 << 20])
+def test_append_batch_matches_single_appends(tmp_path, win):
+    """pom_abuf_append_batch writes the file and returns the locations of
+    single appends in order: records split across windows, a record ending
+    exactly on a window boundary, empty records, and a second batch after a
+    single append."""
+    recs = _records(9, seed=5)
+    lens = [itb.header_fields(r)[0] for r in recs]
+    lens[2] = 0
+    lens[4] = win - sum(lens[:4]) % win if win < 2 * max(lens) else lens[4]
+    lens[4] = min(lens[4], len(recs[4]))
+    single, batch = str(tmp_path / "single"), str(tmp_path / "batch")
+    a = itb.AppendFile(single, win=win)
+    want = [a.append(r, n) for r, n in zip(recs, lens)] + [a.append(bytes(recs[0][:777]))]
+    want += [a.append(r, n) for r, n in zip(recs[:3], lens[:3])]
+    a.close()
+    b = itb.AppendFile(batch, win=win)
+    got = b.append_batch(recs, lens) + [b.append(bytes(recs[0][:777]))]
+    got += b.append_batch(recs[:3], lens[:3])
+    assert b.append_batch([]) == []
+    b.close()
+    assert got == want
+    assert open(batch, "rb").read() == open(single, "rb").read()
+
+
 def _expected_compress(oracle, rec):
     """itb_lzo_compress, restated: returns (which, expected oi record bytes)."""
     ln = itb.header_fields(rec)[0]
