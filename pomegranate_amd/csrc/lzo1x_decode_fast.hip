@@ -75,6 +75,9 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_RING
 #define POM_RING 4096
 #endif
+#ifndef POM_PRIO
+#define POM_PRIO 2                               // wave priority falls as a block progresses (1: executor, 2: + parser, 3: parser static 3)
+#endif
 #ifndef POM_WIDE
 #define POM_WIDE 1                               // 16-byte steps for batches of contiguous / period-1 ops
 #endif
@@ -185,6 +188,22 @@ __device__ __forceinline__ uint32_t lds_load(const uint32_t* p)
 __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// s_setprio takes an immediate: 3 for the first quarter of a block's output
+// (input, for the parser), down to 0 for the last.  Waves of a CU's blocks
+// that fall behind then win issue arbitration over those ahead, so the blocks
+// of a single-round launch finish together instead of draining one by one
+// (age priority alone favours the oldest waves).
+__device__ __forceinline__ void prio_by_progress(uint32_t done, uint32_t total)
+{
+    const uint32_t q = (uint32_t)(((uint64_t)done * 4u) / ((uint64_t)total + 1u));
+    switch (__builtin_amdgcn_readfirstlane(q)) {
+    case 0: __builtin_amdgcn_s_setprio(3); break;
+    case 1: __builtin_amdgcn_s_setprio(2); break;
+    case 2: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+    }
 }
 
 struct Blk {
@@ -849,6 +868,8 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
                 total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u);
 #endif
         lds_store(&S.parsed, q + 1);
+        if (POM_PRIO == 2)
+            prio_by_progress(k.P, k.z);
         STAMP(PH_WRITE);
         if (err || eof)
             break;
@@ -1065,6 +1086,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
     uint32_t reason = refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
     if (wave == 1) {
+        if (POM_PRIO == 3)
+            __builtin_amdgcn_s_setprio(3);
 #ifdef POM_EXPERIMENT_REPLAY
         // (timing experiment only: publish the recorded pieces at once, then
         // only the writer duty runs)
@@ -1515,6 +1538,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 s = e;
             }
             carry += wtotal;
+            if (POM_PRIO >= 1)
+                prio_by_progress(carry, k.cap);
             wave_order();
         }
         w0 += kWave;
