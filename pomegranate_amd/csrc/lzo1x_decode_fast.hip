@@ -76,7 +76,7 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #define POM_RING 4096
 #endif
 #ifndef POM_PRIO
-#define POM_PRIO 2                               // wave priority falls as a block progresses (1: executor, 2: + parser, 3: parser static 3)
+#define POM_PRIO 3                               // executor priority falls as its block progresses; 3: parser static 3 (2: parser by input)
 #endif
 #ifndef POM_WIDE
 #define POM_WIDE 1                               // 16-byte steps for batches of contiguous / period-1 ops
@@ -197,7 +197,9 @@ __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
 // (age priority alone favours the oldest waves).
 __device__ __forceinline__ void prio_by_progress(uint32_t done, uint32_t total)
 {
-    const uint32_t q = (uint32_t)(((uint64_t)done * 4u) / ((uint64_t)total + 1u));
+    uint32_t q = (uint32_t)(((uint64_t)done * 4u) / ((uint64_t)total + 1u));
+    if (POM_PRIO == 4)                               // (variant: 2, 2, 1, 0 under a parser at 3)
+        q = q == 0 ? 1u : q;
     switch (__builtin_amdgcn_readfirstlane(q)) {
     case 0: __builtin_amdgcn_s_setprio(3); break;
     case 1: __builtin_amdgcn_s_setprio(2); break;
@@ -1086,7 +1088,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
     uint32_t reason = refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
     if (wave == 1) {
-        if (POM_PRIO == 3)
+        if (POM_PRIO >= 3)
             __builtin_amdgcn_s_setprio(3);
 #ifdef POM_EXPERIMENT_REPLAY
         // (timing experiment only: publish the recorded pieces at once, then
@@ -1538,7 +1540,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 s = e;
             }
             carry += wtotal;
-            if (POM_PRIO >= 1)
+            if (POM_PRIO >= 1 && POM_PRIO != 5)            // (variant 5: parser 3 only)
                 prio_by_progress(carry, k.cap);
             wave_order();
         }
