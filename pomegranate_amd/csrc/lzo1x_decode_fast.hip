@@ -76,7 +76,7 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #define POM_RING 4096
 #endif
 #ifndef POM_PRIO
-#define POM_PRIO 3                               // executor priority falls as its block progresses; 3: parser static 3 (2: parser by input)
+#define POM_PRIO 1                               // final-round blocks: parser at priority 3, executor 3..0 by bytes left
 #endif
 #ifndef POM_WIDE
 #define POM_WIDE 1                               // 16-byte steps for batches of contiguous / period-1 ops
@@ -190,20 +190,24 @@ __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// s_setprio takes an immediate: 3 for the first quarter of a block's output
-// (input, for the parser), down to 0 for the last.  Waves of a CU's blocks
-// that fall behind then win issue arbitration over those ahead, so the blocks
-// of a single-round launch finish together instead of draining one by one
-// (age priority alone favours the oldest waves).
-__device__ __forceinline__ void prio_by_progress(uint32_t done, uint32_t total)
+// Drain of the last round of blocks.  Arbitration by age lets the oldest
+// waves of a CU run ahead; the blocks then finish one by one and the last few
+// waves cannot fill their SIMDs.  In the final round (blockIdx >= prio_from)
+// the executor's priority follows the output bytes it has left: 3 while 48 KiB
+// or more remain, then 2, 1 and 0 below 16 KiB, so blocks that are behind win
+// issue over those ahead and a CU's blocks finish together; the longest
+// remaining block goes first.  The parser wave (also the block's HBM writer)
+// stays at 3 so that it keeps ahead of its executor.  Earlier rounds keep the
+// default priority: with blocks queued behind them, finishing early is
+// what frees a slot (C4: 330 vs 300-315 GiB/s with priority everywhere).
+__device__ __forceinline__ void prio_by_bytes_left(uint32_t left)
 {
-    uint32_t q = (uint32_t)(((uint64_t)done * 4u) / ((uint64_t)total + 1u));
-    if (POM_PRIO == 4)                               // (variant: 2, 2, 1, 0 under a parser at 3)
-        q = q == 0 ? 1u : q;
-    switch (__builtin_amdgcn_readfirstlane(q)) {
-    case 0: __builtin_amdgcn_s_setprio(3); break;
-    case 1: __builtin_amdgcn_s_setprio(2); break;
-    case 2: __builtin_amdgcn_s_setprio(1); break;
+    const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 49152u ? 3u : left >= 32768u ? 2u
+                                                      : left >= 16384u ? 1u : 0u);
+    switch (q) {
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
     default: __builtin_amdgcn_s_setprio(0); break;
     }
 }
@@ -870,8 +874,6 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
                 total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u);
 #endif
         lds_store(&S.parsed, q + 1);
-        if (POM_PRIO == 2)
-            prio_by_progress(k.P, k.z);
         STAMP(PH_WRITE);
         if (err || eof)
             break;
@@ -1052,12 +1054,13 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
     uint32_t* __restrict__ fallback, uint2* __restrict__ ops, uint32_t nblocks,
-    uint64_t* __restrict__ stamps)
+    uint32_t prio_from, uint64_t* __restrict__ stamps)
 {
     __shared__ FastLds S;
     const uint32_t b = blockIdx.x;
     if (b >= nblocks)
         return;
+    const bool last_round = b >= prio_from;
     const uint32_t l = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x == 0) {
@@ -1088,7 +1091,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
     uint32_t reason = refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
     if (wave == 1) {
-        if (POM_PRIO >= 3)
+        if (POM_PRIO && last_round)
             __builtin_amdgcn_s_setprio(3);
 #ifdef POM_EXPERIMENT_REPLAY
         // (timing experiment only: publish the recorded pieces at once, then
@@ -1540,8 +1543,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 s = e;
             }
             carry += wtotal;
-            if (POM_PRIO >= 1 && POM_PRIO != 5)            // (variant 5: parser 3 only)
-                prio_by_progress(carry, k.cap);
+            if (POM_PRIO && last_round)
+                prio_by_bytes_left(k.cap > carry ? k.cap - carry : 0u);
             wave_order();
         }
         w0 += kWave;
@@ -1577,6 +1580,24 @@ extern "C" size_t lzo_mi355x_fast_ops_bytes_per_block(void)
     return (size_t)kSlots * kOpMax * sizeof(uint2);
 }
 
+// First block of the launch's final round: blocks resident at once are 16
+// per CU (LDS and 8 waves per SIMD).
+static uint32_t prio_from(uint32_t nblocks)
+{
+    static int cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return 0;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            return 0;
+        cus[dev] = n;
+    }
+    const uint64_t resident = (uint64_t)cus[dev] * (2 * POM_WAVES_PER_EU);
+    return nblocks > resident ? (uint32_t)(nblocks - resident) : 0u;
+}
+
 extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint64_t* src_off,
                                                  const uint32_t* src_len, uint8_t* dst,
                                                  const uint64_t* dst_off, const uint32_t* dst_cap,
@@ -1588,7 +1609,7 @@ extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint6
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0,
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
-                       fallback, (uint2*)ops, nblocks, nullptr);
+                       fallback, (uint2*)ops, nblocks, prio_from(nblocks), nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1602,6 +1623,6 @@ extern "C" int lzo_mi355x_debug_decompress_fast_stamps(
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_fast_kernel<true>, dim3(nblocks), dim3(2 * kWave), 0,
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
-                       fallback, (uint2*)ops, nblocks, stamps);
+                       fallback, (uint2*)ops, nblocks, prio_from(nblocks), stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
