@@ -78,6 +78,9 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_PRIO
 #define POM_PRIO 1                               // final-round blocks: parser at priority 3, executor 3..0 by bytes left
 #endif
+#ifndef POM_PRIO_STEP
+#define POM_PRIO_STEP 10240                      // executor priority drops every this many bytes left (swept 4-20 KiB)
+#endif
 #ifndef POM_WIDE
 #define POM_WIDE 1                               // 16-byte steps for batches of contiguous / period-1 ops
 #endif
@@ -193,8 +196,9 @@ __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
 // Drain of the last round of blocks.  Arbitration by age lets the oldest
 // waves of a CU run ahead; the blocks then finish one by one and the last few
 // waves cannot fill their SIMDs.  In the final round (blockIdx >= prio_from)
-// the executor's priority follows the output bytes it has left: 3 while 48 KiB
-// or more remain, then 2, 1 and 0 below 16 KiB, so blocks that are behind win
+// the executor's priority follows the output bytes it has left: 3 while 3 steps
+// (POM_PRIO_STEP, 10 KiB) or more remain, then 2, 1 and 0 below one step, so
+// blocks that are behind win
 // issue over those ahead and a CU's blocks finish together; the longest
 // remaining block goes first.  The parser wave (also the block's HBM writer)
 // stays at 3 so that it keeps ahead of its executor.  Earlier rounds keep the
@@ -202,8 +206,9 @@ __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
 // what frees a slot (C4: 330 vs 300-315 GiB/s with priority everywhere).
 __device__ __forceinline__ void prio_by_bytes_left(uint32_t left)
 {
-    const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 49152u ? 3u : left >= 32768u ? 2u
-                                                      : left >= 16384u ? 1u : 0u);
+    constexpr uint32_t st = POM_PRIO_STEP;
+    const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
+                                                      : left >= st ? 1u : 0u);
     switch (q) {
     case 3: __builtin_amdgcn_s_setprio(3); break;
     case 2: __builtin_amdgcn_s_setprio(2); break;
