@@ -59,7 +59,7 @@ constexpr uint32_t kStageBytes = kPiece + 512;
 constexpr uint32_t kOpMax = (kPiece + 2) / 3 * 2 + 64;
 static_assert(kOpMax < (1u << 16), "piece info: 16-bit op count");
 #ifndef POM_SLOTS
-#define POM_SLOTS 4
+#define POM_SLOTS 8
 #endif
 constexpr uint32_t kSlots = POM_SLOTS;           // parsed pieces the parser may run ahead
 static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");

@@ -82,7 +82,7 @@ for b in np.nonzero(rs)[0][:4]:
     q, w0 = int((rsf[b] >> 4) & 0xFFFFFFF), int(rsf[b] >> 32)
     per = opsbuf.numel() // nb
     slot = opsbuf[b * per: (b + 1) * per].view(torch.int32).view(-1, 2).cpu().numpy()
-    kslots = 4
+    kslots = 8
     ops_q = slot[(q % kslots) * (len(slot) // kslots): (q % kslots + 1) * (len(slot) // kslots)]
     np.save(os.path.join(ROOT, "gpurun_out", f"refused_b{b}_q{q}.npy"), ops_q)
     print("refused block", int(b), "reason", int(rs[b]), "piece", q, "window", w0)
