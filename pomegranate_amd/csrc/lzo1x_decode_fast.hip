@@ -81,6 +81,9 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_PRIO_STEP
 #define POM_PRIO_STEP 10240                      // executor priority drops every this many bytes left (swept 4-20 KiB)
 #endif
+#ifndef POM_PARSER_PRIO
+#define POM_PARSER_PRIO 3                        // final-round parser wave priority
+#endif
 #ifndef POM_WIDE
 #define POM_WIDE 1                               // 16-byte steps for batches of contiguous / period-1 ops
 #endif
@@ -1097,7 +1100,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     uint32_t reason = refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
     if (wave == 1) {
         if (POM_PRIO && last_round)
-            __builtin_amdgcn_s_setprio(3);
+            __builtin_amdgcn_s_setprio(POM_PARSER_PRIO);
 #ifdef POM_EXPERIMENT_REPLAY
         // (timing experiment only: publish the recorded pieces at once, then
         // only the writer duty runs)
