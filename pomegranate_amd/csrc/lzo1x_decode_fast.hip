@@ -9,14 +9,18 @@
 //    (lib/minilzo.c:3308-3699) is a state machine
 //    over instruction starts (pos, state), state A (top), B (after a literal
 //    run) or C (after 1-3 trailing literals).  Every lane decodes
-//    speculatively from kLook bytes before its segment (state A, restarting
-//    one byte later whenever the guess runs into an impossible instruction)
-//    and marks the points it visits inside its segment.  Each lane then walks
-//    the TRUE path from its assumed entry (its predecessor's exit) until it
-//    lands on one of its own marks, and a scalar scan chains the true entries,
-//    walking exactly only where a guess was wrong.  Two more walks count and
-//    write the ops (literal runs and matches: length, source) of the true path
-//    to one of kSlots per-block op slots in global scratch.
+//    speculatively from kLook bytes before its segment (restarting one byte
+//    later whenever the guess runs into an impossible instruction) and keeps
+//    the instruction starts its final attempt visits inside its segment as
+//    per-state bitmaps in registers, plus a bitmap of the starts that yield
+//    two ops (a match and its trailing literals).  Each lane then walks the
+//    TRUE path from its assumed entry (its predecessor's exit) until it lands
+//    on one of its own starts: from there the paths agree, and the bitmaps
+//    give the op count of the rest of the segment (popcounts), so no separate
+//    counting walk is needed.  A scalar scan chains the true entries, walking
+//    exactly only where a guess was wrong.  One more walk per lane writes the
+//    ops (length, source) of the true path to one of kSlots per-block op slots
+//    in global scratch.
 //    Writer duty, between parse steps: copy final output from the LDS ring to
 //    HBM in 1-KiB dwordx4 chunks; publish `issued` (ring slots reusable) at
 //    once and `landed` (readable from HBM) when the executor needs it.
@@ -26,9 +30,16 @@
 //    queue).  Per 64 ops of a published piece: a DPP prefix sum gives output
 //    offsets; literal spans and far match sources are copied into an LDS
 //    source buffer with one batched load round trip; source forwarding and
-//    batches whose match sources all precede the batch; each batch is
-//    produced 256 bytes per step into the LDS output ring (op starts tagged
-//    per 4-byte chunk, a ballot maps every chunk to its op).
+//    batches whose match sources all precede the batch.  Every batch is
+//    produced 1 KiB per step into the LDS output ring: a lane is a 16-byte
+//    chunk of one op (op starts tagged per chunk, a ballot maps every chunk to
+//    its op), read with misaligned ds_read_b128:
+//      - contiguous sources (literals, matches that do not overlap
+//        themselves): one read;
+//      - a match of period p >= 16 whose chunk wraps the period: two reads
+//        (the wrapped part read p bytes lower) merged by a byte mask;
+//      - a match of period 1..15: its pattern, expanded by v_perm with a
+//        selector table indexed by (period, phase).
 //
 // Anything the fast path does not handle exactly (malformed input, lookbehind
 // or capacity errors, op-list overflow, EOF not at the end, misaligned
@@ -44,27 +55,29 @@ namespace {
 
 constexpr int kWave = 64;
 #ifndef POM_SEG
-#define POM_SEG 16
+#define POM_SEG 32
 #endif
 #ifndef POM_LOOK
 #define POM_LOOK 24
 #endif
 constexpr uint32_t kSeg = POM_SEG;               // input bytes per lane per piece
+static_assert(kSeg <= 32, "segment starts are 32-bit bitmaps");
 constexpr uint32_t kLook = POM_LOOK;             // speculative lead-in before a segment
-constexpr uint32_t kPiece = kWave * kSeg;        // 1 KiB of compressed input
-constexpr uint32_t kStageBytes = kPiece + 512;
+static_assert(kLook <= kSeg, "lead-in stays inside the previous segment");
+constexpr uint32_t kPiece = kWave * kSeg;        // 2 KiB of compressed input
+constexpr uint32_t kStageBytes = kPiece + 64;    // + the longest non-extended instruction
 // Ops per piece: an instruction that yields two ops (a match and its 1-3
 // trailing literals) is at least 3 bytes, so a piece holds at most
-// ceil(kPiece / 3) * 2 ops (683 for 1 KiB).
+// ceil(kPiece / 3) * 2 ops.
 constexpr uint32_t kOpMax = (kPiece + 2) / 3 * 2 + 64;
 static_assert(kOpMax < (1u << 16), "piece info: 16-bit op count");
 #ifndef POM_SLOTS
-#define POM_SLOTS 8
+#define POM_SLOTS 4
 #endif
 constexpr uint32_t kSlots = POM_SLOTS;           // parsed pieces the parser may run ahead
 static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_WRITER_SLEEP
-#define POM_WRITER_SLEEP 127                     // idle writer sleeps ~8K cycles between polls
+#define POM_WRITER_SLEEP 32                      // idle writer sleeps ~2K cycles between polls
 #endif
 #ifndef POM_FWD_ROUNDS
 #define POM_FWD_ROUNDS 3                         // source-forwarding rounds per window
@@ -79,19 +92,23 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #define POM_PRIO 1                               // final-round blocks: parser at priority 3, executor 3..0 by bytes left
 #endif
 #ifndef POM_PRIO_STEP
-#define POM_PRIO_STEP 10240                      // executor priority drops every this many bytes left (swept 4-20 KiB)
+#define POM_PRIO_STEP 10240                      // executor priority drops every this many bytes left
 #endif
 #ifndef POM_PARSER_PRIO
 #define POM_PARSER_PRIO 3                        // final-round parser wave priority
 #endif
-#ifndef POM_WIDE
-#define POM_WIDE 1                               // 16-byte steps for batches of contiguous / period-1 ops
+#ifndef POM_LAZY_PUB
+#define POM_LAZY_PUB 1                           // hand output to the writer per completed 1-KiB chunk
+#endif
+#ifndef POM_EXEC_SLEEP
+#define POM_EXEC_SLEEP 4                         // executor waits sleep ~256 cycles between polls
 #endif
 #ifndef POM_DUTY_EVERY
 #define POM_DUTY_EVERY 4                         // parser pass-1 iterations between writer duties
 #endif
 constexpr uint32_t kRing = POM_RING;             // recent output kept in LDS
 constexpr uint32_t kRingMask = kRing - 1;
+constexpr uint32_t kMirror = 32;                 // ring[0, 16) mirrored after its end (+ write spill)
 #ifndef POM_SRCBUF
 #define POM_SRCBUF 1024
 #endif
@@ -104,6 +121,9 @@ constexpr uint32_t kMaxOpLen = 1u << 25;         // 64 ops per window cannot wra
 constexpr int32_t kFallback = 0x7FFF0001;        // status: exact decoder pending
 constexpr uint32_t kInfoEof = 1u << 16;          // piece info: the piece ends with EOF
 constexpr uint32_t kInfoErr = 1u << 17;          // piece info: the block needs the exact decoder
+// A step covers at most 64 chunks of 16 bytes: an op read by a step whose
+// first byte is xs lies at most kStepSpan bytes after xs.
+constexpr uint32_t kStepSpan = 16 * kWave + 16;
 // (diagnostics: why, in bits 20..23 of the piece info / the CN_REASON stamp)
 enum { RS_NONE, RS_OFF_END, RS_BAD, RS_OPS, RS_DEAD, RS_EWAIT, RS_OVERRUN, RS_LOOKBEHIND,
        RS_SPACE, RS_LANDED, RS_HEAD };
@@ -114,20 +134,27 @@ constexpr uint32_t ST_B = 1;   // after a literal run: t < 16 is a 3-byte M1 (di
 constexpr uint32_t ST_C = 2;   // after trailing literals: t < 16 is a 2-byte M1
 constexpr uint32_t ST_F = 3;   // first byte of the stream (lib/minilzo.c:3357)
 constexpr uint32_t kPosEnd = 0xFFFFFFF0u;        // exit marker: EOF reached / dead path
-constexpr uint32_t kGenMax = 31;                 // restart generations a mark can tell apart
-constexpr uint32_t kPosUnknown = 0xFFFFFFE0u;    // speculative walk gave up
+// walk outcome
+constexpr uint32_t FL_OK = 0;                    // reached the segment end
+constexpr uint32_t FL_EOF = 1;                   // EOF at the end of the input
+constexpr uint32_t FL_DEAD = 2;                  // malformed / past the input end without EOF
+constexpr uint32_t FL_UNK = 3;                   // speculative walk gave up (slow instruction)
 
 struct __attribute__((aligned(16))) FastLds {
     // executor
-    uint32_t ring[kRing / 4];
+    uint32_t ring[(kRing + kMirror) / 4];
     uint32_t src[kSrcDw];     // this window's literal spans and far match sources
-    uint4 wop[kWave];         // window op: {o, source base (| kLitFlag: linear), first chunk, L (| kLitFlag: needs HBM)}
+    uint4 wop[kWave];         // window op: {o, source base (| kLitFlag: linear), first 16-B chunk, L}
     uint2 wper[kWave];        // window op: {period, floor((2^32-1)/period)}
     uint32_t flags[kWave];    // per-step chunk tags (src_issue: per-dword byte flags)
-    uint32_t sink;            // target of masked-off byte writes
+    // v_perm selectors of the period-p pattern expansion (p < 16): byte i of
+    // psel[0][p] selects pattern byte i mod p from dwords 1:0 (12 = zero when
+    // it lies in 2:3), psel[1][p] the same from dwords 3:2.  A chunk of phase
+    // r reads its 16 selectors at offset r (lib/minilzo.c:3622-3646 is the
+    // byte-serial copy this replaces).
+    uint32_t psel[2][16][8];
     // parser
     uint32_t stage[kStageBytes / 4];
-    uint8_t marks[kPiece];    // speculative path marks (pass 1, merge)
     // hand-off words (LDS, workgroup scope)
     uint32_t produced;        // executor -> writer: output bytes final in the ring
     uint32_t issued;          // writer -> executor: stores issued (ring slots reusable)
@@ -140,16 +167,15 @@ struct __attribute__((aligned(16))) FastLds {
 };
 
 constexpr uint32_t kRingOff = 0;                                  // offsetof(FastLds, ring)
-constexpr uint32_t kSrcOff = kRing;                               // offsetof(FastLds, src)
+constexpr uint32_t kSrcOff = kRing + kMirror;                     // offsetof(FastLds, src)
 static_assert(offsetof(FastLds, ring) == kRingOff, "layout");
 static_assert(offsetof(FastLds, src) == kSrcOff, "layout");
-constexpr uint32_t kSinkOff = kSrcOff + kSrcBytes + (kWave * (16 + 8 + 4));   // offsetof(FastLds, sink)
-static_assert(offsetof(FastLds, sink) == kSinkOff, "layout");
 constexpr uint32_t kLdsMask = 0x3FFF;                              // LDS-linear address space
 static_assert(sizeof(FastLds) <= kLdsMask + 1 && kLdsMask + 1 == kLinHbm,
               "linear LDS addresses are masked to 16 KiB");
 // 16 blocks per CU share its 160 KiB of LDS
 static_assert(sizeof(FastLds) * 2 * POM_WAVES_PER_EU <= 160 * 1024, "LDS budget");
+
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
@@ -200,13 +226,11 @@ __device__ __forceinline__ void lds_store(uint32_t* p, uint32_t v)
 // waves of a CU run ahead; the blocks then finish one by one and the last few
 // waves cannot fill their SIMDs.  In the final round (blockIdx >= prio_from)
 // the executor's priority follows the output bytes it has left: 3 while 3 steps
-// (POM_PRIO_STEP, 10 KiB) or more remain, then 2, 1 and 0 below one step, so
-// blocks that are behind win
-// issue over those ahead and a CU's blocks finish together; the longest
-// remaining block goes first.  The parser wave (also the block's HBM writer)
-// stays at 3 so that it keeps ahead of its executor.  Earlier rounds keep the
-// default priority: with blocks queued behind them, finishing early is
-// what frees a slot (C4: 330 vs 300-315 GiB/s with priority everywhere).
+// (POM_PRIO_STEP) or more remain, then 2, 1 and 0 below one step, so blocks
+// that are behind win issue over those ahead and a CU's blocks finish
+// together.  The parser wave (also the block's HBM writer) stays at 3 so that
+// it keeps ahead of its executor.  Earlier rounds keep the default priority:
+// with blocks queued behind them, finishing early is what frees a slot.
 __device__ __forceinline__ void prio_by_bytes_left(uint32_t left)
 {
     constexpr uint32_t st = POM_PRIO_STEP;
@@ -273,7 +297,9 @@ __device__ __forceinline__ uint32_t read_ext(const FastLds& s, const Blk& k, uin
     return v;
 }
 
-__device__ __noinline__ Step decode_one(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st)
+// (k by value: a noinline callee reached from divergent code must not read
+// its arguments from the caller's scratch)
+__device__ __noinline__ Step decode_one(const FastLds& s, const Blk k, uint32_t pos, uint32_t st)
 {
     Step r;
     r.aL = r.bL = 0;
@@ -364,7 +390,7 @@ __device__ __noinline__ Step decode_one(const FastLds& s, const Blk& k, uint32_t
 
 // Branch-free form of decode_one for the common case: the instruction lies in
 // the staged input and any length extension is a single non-zero byte.  One
-// LDS round trip (three aligned dwords -> 8 bytes at pos), then selects; lanes
+// LDS round trip (two aligned dwords -> 4 bytes at pos), then selects; lanes
 // decoding different instruction kinds do not diverge.  Falls back to
 // decode_one otherwise (long extensions, input beyond the staging window).
 // SPEC: speculative use -- never take the slow path; report it as `slow`
@@ -446,20 +472,26 @@ __device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t sh
 // unaligned mode: ds_read_b128 / ds_write_b128 / b64 / b32 / b16 at any byte
 // address are exact (scripts/probe/lds_misaligned_probe.hip; ~1.5x the
 // latency of an aligned access).  The compiler assumes natural alignment for
-// its own accesses, so these are written out.  The read waits for its data
-// itself; LDS accesses of one wave complete in order, so the compiler's own
-// lgkmcnt waits stay correct (they only become more conservative).
+// its own accesses, so these are written out.  The reads wait for their data
+// themselves; LDS accesses of one wave complete in order, so the compiler's
+// own lgkmcnt waits stay correct (they only become more conservative).
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t lds_off(const void* p)
 {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
-__device__ __forceinline__ uint4 lds_read16(uint32_t a)
+__device__ __forceinline__ void lds_read16x4(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                             uint4& va, uint4& vb, uint4& vc, uint4& vd)
 {
-    v4u32 v;
-    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-    return make_uint4(v.x, v.y, v.z, v.w);
+    v4u32 x, y, z, w;
+    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\t"
+                 "ds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(x), "=&v"(y), "=&v"(z), "=&v"(w) : "v"(a), "v"(b), "v"(c), "v"(d) : "memory");
+    va = make_uint4(x.x, x.y, x.z, x.w);
+    vb = make_uint4(y.x, y.y, y.z, y.w);
+    vc = make_uint4(z.x, z.y, z.z, z.w);
+    vd = make_uint4(w.x, w.y, w.z, w.w);
 }
 __device__ __forceinline__ void lds_write16(uint32_t a, uint4 v)
 {
@@ -484,11 +516,43 @@ __device__ __forceinline__ void lds_write1(uint32_t a, uint32_t v)
     asm volatile("ds_write_b8 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
+// The first len (<= 16) bytes of v at LDS address a: one b128 for a whole
+// chunk, else b64/b32/b16/b8 pieces.
+__device__ __forceinline__ void lds_write_part(uint32_t a, uint4 v, uint32_t len)
+{
+#ifdef POM_BYTE_WRITES
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++)
+        if (i < len)
+            lds_write1(a + i, w[i >> 2] >> (8 * (i & 3)));
+    return;
+#endif
+    if (len == 16u) {
+        lds_write16(a, v);
+        return;
+    }
+    uint32_t w0 = v.x, w1 = v.y, ad = a;
+    if (len & 8u) {
+        lds_write8(ad, v.x, v.y);
+        w0 = v.z;
+        w1 = v.w;
+        ad += 8;
+    }
+    if (len & 4u) {
+        lds_write4(ad, w0);
+        w0 = w1;
+        ad += 4;
+    }
+    if (len & 2u) {
+        lds_write2(ad, w0);
+        w0 >>= 16;
+        ad += 2;
+    }
+    if (len & 1u)
+        lds_write1(ad, w0);
+}
 
-
-// 4 bytes at an arbitrary global address via two aligned dword loads (an
-// aligned dword that overlaps valid bytes never leaves their page).  NT: L2
-// served (the vector L1 is not coherent with this wave's earlier stores).
 typedef __attribute__((address_space(1))) const uint32_t gdword;
 
 // 4 bytes at an arbitrary global address via two aligned dword loads (an
@@ -515,53 +579,106 @@ __device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
     return sh ? funnel(w0, w1, sh) : w0;
 }
 
-__device__ __forceinline__ uint32_t global_byte_nt(const uint8_t* p)
+// Bytes [lo, hi) (hi <= 16) of the 16 at global address p, read through L2
+// with aligned dword loads that each hold at least one of those bytes (so no
+// load leaves their pages); the other bytes read as 0.
+__device__ __forceinline__ uint4 global_read16(const uint8_t* p, uint32_t lo, uint32_t hi)
 {
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t w = __builtin_nontemporal_load((gdword*)(a & ~(uintptr_t)3));
-    return (w >> (8u * (uint32_t)(a & 3))) & 0xFFu;
+    gdword* q = (gdword*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t w[5];
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        // aligned dword i holds bytes 4i - sh .. 4i + 3 - sh of the span
+        const bool use = 4 * i < hi + sh && 4 * i + 4 > lo + sh;
+        w[i] = use ? __builtin_nontemporal_load(q + i) : 0u;
+    }
+    uint4 v;
+    v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+    v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+    v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+    return v;
 }
 
+// ---------------------------------------------------------------------------
+// Parser walks.  A lane's final speculative attempt leaves, per state, a
+// bitmap of the instruction starts it visited in its segment [c0, c0 + kSeg)
+// and a bitmap of those starts that yield two ops.  A walk of the true path
+// that lands on one of them follows the speculative path from there: its op
+// count is the popcount of the starts at or after that point (plus the
+// two-op starts), and its exit is the speculative exit.
+// ---------------------------------------------------------------------------
+struct Marks {
+    uint32_t m[4];          // instruction starts, per state (A, B, C, F)
+    uint32_t two;           // starts that yield two ops
+    uint32_t xpos, xst;     // the speculative exit
+};
+
+struct WalkRes {
+    uint32_t pos, st, cnt, fl;
+};
+
+__device__ __forceinline__ uint32_t mark_of(const Marks& M, uint32_t st)
+{
+    return st == ST_A ? M.m[0] : st == ST_B ? M.m[1] : st == ST_C ? M.m[2] : M.m[3];
+}
 
 template <bool SPEC>
-__device__ __forceinline__ uint32_t walk_uniform(const FastLds& S, const Blk& k, uint32_t c0,
-                                                 uint32_t c1, uint32_t gen, uint32_t xpos,
-                                                 uint32_t xst, uint32_t& pos, uint32_t& st)
+__device__ __forceinline__ WalkRes walk_true(const FastLds& S, const Blk& k, uint32_t c0, uint32_t c1,
+                                             const Marks& M, uint32_t pos, uint32_t st)
 {
-    uint32_t steps = 0;                      // (diagnostics)
+    WalkRes w;
+    w.cnt = 0;
+    w.fl = FL_OK;
     while (pos < c1) {
-        steps++;
         if (pos >= k.z) {
+            w.fl = FL_DEAD;
             pos = kPosEnd;
-            st = 0;
-            return steps;
+            break;
         }
-        if (pos >= c0 && S.marks[pos - k.P] == ((st + 1) | (gen << 3))) {
-            pos = xpos;
-            st = xst;
-            return steps;
+        if (pos >= c0) {
+            const uint32_t bit = 1u << (pos - c0);
+            if (mark_of(M, st) & bit) {            // joined the speculative path
+                const uint32_t from = ~(bit - 1u);
+                const uint32_t starts = M.m[0] | M.m[1] | M.m[2] | M.m[3];
+                w.cnt += (uint32_t)__builtin_popcount(starts & from) + (uint32_t)__builtin_popcount(M.two & from);
+                pos = M.xpos;
+                st = M.xst;
+                if (pos == kPosEnd)
+                    w.fl = FL_DEAD;                // it runs off the input end
+                break;
+            }
         }
         bool slow = false;
         const Step r = decode_step<SPEC>(S, k, pos, st, &slow);
         if (SPEC && slow) {
-            pos = kPosUnknown;
-            st = 0;
-            return steps;
+            w.fl = FL_UNK;
+            break;
         }
-        if (r.bad || r.eof) {
+        if (r.eof) {
+            w.fl = r.bad ? FL_DEAD : FL_EOF;
             pos = kPosEnd;
-            st = 0;
-            return steps;
+            break;
         }
+        if (r.bad) {
+            w.fl = FL_DEAD;
+            pos = kPosEnd;
+            break;
+        }
+        w.cnt += (r.aL ? 1u : 0u) + (r.bL ? 1u : 0u);
         pos = r.pos;
         st = r.st;
     }
-    return steps;
+    w.pos = pos;
+    w.st = st;
+    return w;
 }
 
 // Diagnostic build only (STAMPS): per-phase s_memtime cycle sums and event
 // counts go to stamps[b * kStampSlots + i]; no output value depends on them.
-// Each wave writes only the slots it owns (parser: kParserSlots).
+// Each wave writes only the slots it owns (parser: parser_slot).
 // scripts/diag_decode.py knows this order.
 enum { PH_STAGE, PH_PASS1, PH_PWALK, PH_MERGE, PH_COUNT, PH_WRITE, PH_PSLOT, PH_PDUTY,
        PH_EWAIT, PH_WLOAD, PH_WSCAN, PH_FARI, PH_FWD, PH_FARC, PH_BATCH,
@@ -644,7 +761,7 @@ __device__ __forceinline__ uint32_t writer_duty(FastLds& S, uint8_t* out, uint32
 // ---------------------------------------------------------------------------
 template <bool STAMPS>
 __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict__ gops, uint32_t l,
-                            uint64_t* acc)
+                                            uint64_t* acc)
 {
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     WState w;
@@ -659,7 +776,7 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
         for (uint32_t spin = 0; q - lds_load(&S.consumed) >= kSlots; spin++) {
             if (writer_duty(S, k.out, l, w) == 2 || spin > (1u << 22))
                 return;                        // the executor refused (or is stuck)
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
         }
         STAMP(PH_PSLOT);
         if (STAMPS)
@@ -684,38 +801,42 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
                         v |= (uint32_t)base[j] << (8 * (j - i));
                 S.stage[i >> 2] = v;
             }
-            for (uint32_t i = l * 4; i < kPiece; i += kWave * 4)
-                *(uint32_t*)&S.marks[i] = 0;
             wave_order();
             STAMP(PH_STAGE);
             const uint32_t c0 = k.P + l * kSeg;        // this lane's segment
             const uint32_t c1 = c0 + kSeg;
 
-            // ---- pass 1: speculative walk, mark visited points ---------------
-            // A mark is (state + 1) | (gen << 3) -- state + 1 takes 3 bits, ST_F
-            // included; gen counts this lane's restarts, and only marks of the
-            // final generation lie on the path that really reaches xpos (a
-            // restart breaks the chain).
+            // ---- pass 1: speculative walk; the final attempt's starts -----------
             const bool p1 = c1 > entry_pos;            // else no instruction starts here
             uint32_t pos = c0 >= k.P + kLook ? c0 - kLook : k.P;
             if (pos < entry_pos)
                 pos = entry_pos;
             uint32_t st = pos == entry_pos ? entry_st : ST_A;
-            uint32_t gen = 0;
+            Marks M;
+            M.m[0] = M.m[1] = M.m[2] = M.m[3] = 0;
+            M.two = 0;
             for (uint32_t it = 1;; it++) {
                 const bool act = p1 && pos < c1 && pos < k.z;
                 if (!wave_ballot(act))
                     break;
                 if (act) {
-                    if (pos >= c0)
-                        S.marks[pos - k.P] = (uint8_t)((st + 1) | (gen << 3));
                     bool slow = false;
                     const Step r = decode_step<true>(S, k, pos, st, &slow);
+                    const bool mine = pos >= c0;
+                    const uint32_t bit = mine ? 1u << (pos - c0) : 0u;
                     if (r.bad || r.eof) {              // impossible guess: restart later
                         pos++;
                         st = ST_A;
-                        gen = gen < kGenMax ? gen + 1 : kGenMax;
+                        if (mine) {                    // only the final attempt counts
+                            M.m[0] = M.m[1] = M.m[2] = M.m[3] = 0;
+                            M.two = 0;
+                        }
                     } else {
+                        M.m[0] |= st == ST_A ? bit : 0u;
+                        M.m[1] |= st == ST_B ? bit : 0u;
+                        M.m[2] |= st == ST_C ? bit : 0u;
+                        M.m[3] |= st == ST_F ? bit : 0u;
+                        M.two |= r.bL ? bit : 0u;
                         pos = r.pos;
                         st = r.st;
                     }
@@ -729,131 +850,163 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
                     STAMP(PH_PDUTY);
                 }
             }
-            const uint32_t xpos = !p1 ? entry_pos : pos >= k.z ? kPosEnd : pos;
-            const uint32_t xst = !p1 ? entry_st : st;
-            const uint32_t xgen = !p1 ? 0u : gen < kGenMax ? gen : 0xFFu;   // saturated: never merge
+            M.xpos = !p1 ? entry_pos : pos >= k.z ? kPosEnd : pos;
+            M.xst = !p1 ? entry_st : st;
             wave_order();
             STAMP(PH_PASS1);
 
             // ---- true entries: one parallel walk from the assumed entries, then
             // a scalar scan that reuses it and walks only where the guess was wrong.
-            const uint32_t apos = shift_up1(xpos, entry_pos), ast = shift_up1(xst, entry_st);
-            uint32_t fpos = apos, fst = ast;
-            {
-                const uint32_t ws = walk_uniform<true>(S, k, c0, c1, xgen, xpos, xst, fpos, fst);
-                if (STAMPS)
-                    acc[CN_IT_PWALK] += wave_max_dbg(ws);
-            }
+            const uint32_t apos = shift_up1(M.xpos, entry_pos), ast = shift_up1(M.xst, entry_st);
+            const WalkRes f = walk_true<true>(S, k, c0, c1, M, apos, ast);
             STAMP(PH_PWALK);
             if (writer_duty(S, k.out, l, w) == 2)
                 return;
             STAMP(PH_PDUTY);
-            // Where lane i's true entry E equals its assumed one, lanes i, i+1,
-            // ... stay right as long as each walk landed on the next lane's
-            // assumed entry (f_l == x_l) and none gave up, so the scan jumps to
-            // the first lane q where that fails: mm (lane q-1's walk missed lane
-            // q's assumed entry) or uk (lane q's own walk gave up), E_q = f_{q-1}.
-            uint32_t epos = apos, est = ast;
+            // Where lane i's true entry E equals its assumed one and its walk
+            // finished, lanes i, i+1, ... stay right as long as each walk ended
+            // at the next lane's assumed entry (f_l == x_l, FL_OK) and that
+            // lane's own walk finished; the scan jumps to the first lane q
+            // where that fails, E_q = f_{q-1}.
+            uint32_t epos = kPosEnd, est = ST_A, ecnt = 0;
+            uint64_t run = 0;                          // lanes whose parallel walk is true
+            bool dead = false;
+#ifdef POM_DEBUG_DEAD
+            bool dbg_stage_bad = false;
+#endif
             {
-                const uint64_t mm = wave_ballot(fpos != xpos || fst != xst) << 1;
-                const uint64_t uk = wave_ballot(fpos == kPosUnknown);
+                const uint64_t brk = wave_ballot(f.fl != FL_OK || f.pos != M.xpos || f.st != M.xst) << 1;
+                const uint64_t unk = wave_ballot(f.fl == FL_UNK);
                 uint32_t E = entry_pos, Est = entry_st;
                 uint32_t i = 0;
+#ifdef POM_DEBUG_DEAD
+                uint32_t dbg_i = 99, dbg_E = 0, dbg_Est = 0;
+                (void)dbg_i; (void)dbg_E; (void)dbg_Est;
+#endif
                 while (i < (uint32_t)kWave) {
-                    if (E == lane_read(apos, i) && Est == lane_read(ast, i)) {
-                        const uint64_t from_i = ~0ull << i;
-                        const uint64_t cand = (mm & (from_i << 1)) | (uk & from_i);
-                        if (!cand) {                   // right through lane 63
-                            E = lane_read(fpos, kWave - 1);
-                            Est = lane_read(fst, kWave - 1);
+                    const uint32_t ci1 = k.P + (i + 1) * kSeg;
+                    if (E >= ci1) {                    // no true start in segment i
+                        const uint32_t j = E - k.P < kPiece ? (E - k.P) / kSeg : (uint32_t)kWave;
+                        i = j > i + 1 ? j : i + 1;
+                        continue;
+                    }
+                    if (E == lane_read(apos, i) && Est == lane_read(ast, i) && !((unk >> i) & 1)) {
+                        const uint64_t cand = i + 1 < (uint32_t)kWave ? (brk | unk) & (~0ull << (i + 1)) : 0ull;
+                        const uint32_t qq = cand ? (uint32_t)__builtin_ctzll(cand) : (uint32_t)kWave;
+                        run |= (qq == 64 ? ~0ull : ((1ull << qq) - 1)) & (~0ull << i);
+                        E = lane_read(f.pos, qq - 1);
+                        Est = lane_read(f.st, qq - 1);
+                        const uint32_t fl = lane_read(f.fl, qq - 1);
+                        if (fl == FL_EOF) {
+                            eof = true;
                             break;
                         }
-                        const uint32_t qq = (uint32_t)__builtin_ctzll(cand);
-                        if (qq > i) {
-                            E = lane_read(fpos, qq - 1);
-                            Est = lane_read(fst, qq - 1);
-                            i = qq;
+                        if (fl == FL_DEAD) {
+                            dead = true;
+#ifdef POM_DEBUG_DEAD
+                            dbg_i = 100 + qq - 1;
+#endif
+                            break;
                         }
+                        i = qq;
+                        continue;
                     }
                     // lane i on its own, from its true entry E
+                    Marks Mi;
+                    Mi.m[0] = lane_read(M.m[0], i);
+                    Mi.m[1] = lane_read(M.m[1], i);
+                    Mi.m[2] = lane_read(M.m[2], i);
+                    Mi.m[3] = lane_read(M.m[3], i);
+                    Mi.two = lane_read(M.two, i);
+                    Mi.xpos = lane_read(M.xpos, i);
+                    Mi.xst = lane_read(M.xst, i);
+#ifdef POM_DEBUG_DEAD
+                    dbg_E = E;
+                    dbg_Est = Est;
+#endif
+                    const WalkRes g = walk_true<false>(S, k, ci1 - kSeg, ci1, Mi, E, Est);
+                    if (STAMPS)
+                        acc[CN_WALKS] += 1;
                     if (l == i) {
                         epos = E;
                         est = Est;
+                        ecnt = g.cnt;
                     }
-                    const uint32_t ci1 = k.P + (i + 1) * kSeg;
-                    if (E < ci1) {                     // else: segment i has no true start
-                        if (E == lane_read(apos, i) && Est == lane_read(ast, i) &&
-                            lane_read(fpos, i) != kPosUnknown) {
-                            E = lane_read(fpos, i);
-                            Est = lane_read(fst, i);
-                        } else {
-                            const uint32_t ws = walk_uniform<false>(S, k, ci1 - kSeg, ci1, lane_read(xgen, i),
-                                                                    lane_read(xpos, i), lane_read(xst, i), E, Est);
-                            if (STAMPS) {
-                                acc[CN_WALKS] += 1;
-                                acc[CN_IT_WALK] += ws;
-                            }
-                            STAMP(PH_MERGE);
-                            if (writer_duty(S, k.out, l, w) == 2)
-                                return;
-                            STAMP(PH_PDUTY);
-                        }
+                    E = g.pos;
+                    Est = g.st;
+                    STAMP(PH_MERGE);
+                    if (writer_duty(S, k.out, l, w) == 2)
+                        return;
+                    STAMP(PH_PDUTY);
+                    if (g.fl == FL_EOF) {
+                        eof = true;
+                        break;
+                    }
+                    if (g.fl == FL_DEAD) {
+                        dead = true;
+#ifdef POM_DEBUG_DEAD
+                        dbg_i = i;
+#endif
+                        break;
                     }
                     i++;
                 }
                 next_pos = E;                          // (uniform: the piece's true exit)
                 next_st = Est;
+#ifdef POM_DEBUG_DEAD
+                if (dead || (!eof && E == kPosEnd)) {
+                    // (diagnostic) does the LDS stage still hold the input?
+                    bool diff = false;
+                    for (uint32_t i = l * 4; i < kStageBytes; i += kWave * 4) {
+                        uint32_t v = 0;
+                        if (i + 4 <= k.staged)
+                            v = global_dword<false>(k.in + k.P + i);
+                        else
+                            for (uint32_t j = i; j < k.staged; j++)
+                                v |= (uint32_t)k.in[k.P + j] << (8 * (j - i));
+                        diff |= S.stage[i >> 2] != v;
+                    }
+                    dbg_stage_bad = wave_ballot(diff) != 0;
+                }
+#endif
+                if ((run >> l) & 1) {
+                    epos = apos;
+                    est = ast;
+                    ecnt = f.cnt;
+                }
             }
             STAMP(PH_MERGE);
-
-            // ---- pass 3: count ops of the true path ------------------------------
-            uint32_t nops = 0;
-            bool lane_eof = false, lane_err = false;
-            {
-                uint32_t p = epos, s = est;
-                uint32_t itc = 0;
-                while (p < c1) {
-                    itc++;
-                    const Step r = decode_step(S, k, p, s);
-                    if (r.bad) {
-                        lane_err = true;
-                        break;
-                    }
-                    if (r.eof) {                       // EOF carries no op
-                        lane_eof = true;
-                        break;
-                    }
-                    if (r.aL > kMaxOpLen || r.bL > kMaxOpLen) {
-                        lane_err = true;
-                        break;
-                    }
-                    nops += (r.aL ? 1u : 0u) + (r.bL ? 1u : 0u);
-                    p = r.pos;
-                    s = r.st;
-                }
-                if (STAMPS)
-                    acc[CN_IT_COUNT] += wave_max_dbg(itc);
-            }
-            const uint32_t incl = wave_incl_scan(nops);
+            const uint32_t incl = wave_incl_scan(ecnt);
             total_ops = lane_read(incl, kWave - 1);
-            err = wave_ballot(lane_err) != 0 || total_ops > kOpMax;
-            if (err)
-                reason = wave_ballot(lane_err) != 0 ? RS_BAD : RS_OPS;
-            eof = wave_ballot(lane_eof) != 0;
-            STAMP(PH_COUNT);
-            if (writer_duty(S, k.out, l, w) == 2)
-                return;
-            STAMP(PH_PDUTY);
-            // ---- pass 4: write the ops (length, source) to the slot ---------------
+            if (dead) {
+                err = true;
+                reason = RS_DEAD;
+#ifdef POM_DEBUG_DEAD
+                if (dbg_stage_bad)
+                    reason = 12;                       // (diagnostic) the stage was overwritten
+#endif
+            } else if (total_ops > kOpMax) {
+                err = true;
+                reason = RS_OPS;
+            }
+            // ---- write the ops (length, source) of the true path to the slot ------
             if (!err) {
-                uint32_t wi = incl - nops;
+                uint32_t wi = incl - ecnt;
+                const uint32_t wend = incl;
                 uint32_t p = epos, s = est;
+                bool lane_err = false;
                 uint32_t itw = 0;
-                while (p < c1) {
+                while (p < c1 && wi < wend) {
                     itw++;
                     const Step r = decode_step(S, k, p, s);
-                    if (r.eof)
+                    if (r.eof || r.bad) {
+                        lane_err = true;               // (the scan saw ops here)
                         break;
+                    }
+                    if (r.aL > kMaxOpLen || r.bL > kMaxOpLen || wi + (r.aL ? 1u : 0u) + (r.bL ? 1u : 0u) > wend) {
+                        lane_err = true;
+                        break;
+                    }
                     if (r.aL)
                         slot[wi++] = make_uint2(r.aL, r.aS);
                     if (r.bL)
@@ -861,8 +1014,13 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
                     p = r.pos;
                     s = r.st;
                 }
+                lane_err = lane_err || wi != wend;
                 if (STAMPS)
                     acc[CN_IT_WRITE] += wave_max_dbg(itw);
+                if (wave_ballot(lane_err)) {
+                    err = true;
+                    reason = RS_BAD;
+                }
             }
             if (!err && !eof && next_pos == kPosEnd) {
                 err = true;                            // dead without EOF
@@ -874,13 +1032,6 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
         __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0)
         lds_store(&S.pinfo[q & (kSlots - 1)],
                   total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u) | (reason << 20));
-#ifdef POM_EXPERIMENT_RECORD
-        // (timing experiment only: every piece keeps its slot; the piece
-        // infos go to the last slot for an executor-only replay)
-        if (l == 0)
-            ((uint32_t*)(gops + (kSlots - 1) * kOpMax))[q] =
-                total_ops | (eof ? kInfoEof : 0u) | (err ? kInfoErr : 0u);
-#endif
         lds_store(&S.parsed, q + 1);
         STAMP(PH_WRITE);
         if (err || eof)
@@ -907,8 +1058,8 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
 // copied into S.src once per window -- one batched global round trip -- and
 // then read LDS like everything else.  Literal spans come first (they are
 // short), then far sources, each class a prefix in window order while the
-// buffer lasts.  Ops that do not fit read HBM byte by byte in their steps:
-// literals through linear addresses from kLinHbm (input position + kLinHbm).
+// buffer lasts.  Ops that do not fit read HBM in their steps: literals
+// through linear addresses from kLinHbm (input position + kLinHbm).
 //
 // Where output bytes are (carry = output before this window): the ring holds
 // every position >= carry - kRing, and the executor waited for `landed` >=
@@ -931,11 +1082,11 @@ __device__ __forceinline__ uint32_t wait_landed(FastLds& S, uint32_t need, uint3
         return seen;
     lds_store(&S.need, need);
     for (uint32_t spin = 0; seen < need; spin++) {
-        if (spin > (1u << 22)) {               // writer stuck: let the exact path redo it
+        if (spin > (1u << 20)) {               // writer stuck: let the exact path redo it
             refuse = true;
             break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(POM_EXEC_SLEEP);
         seen = lds_load(&S.landed);
     }
     return seen;
@@ -959,10 +1110,11 @@ __device__ __forceinline__ SrcCopy src_issue(FastLds& S, const Blk& k, uint32_t 
     fc.miss = false;
     const uint32_t span = dp ? dp : L;
     const bool litc = l < nwin && lit && L != 0;
-    // some byte may read below the ring: sp + kRing < step_end + 4 with
-    // step_end <= x + 259 and sp - db <= x - o (p == 0) or < p
+    // some byte may be read from below the ring: a step starting at xs reads
+    // the ring down to xs - kRing, and the step of the op's last chunk starts
+    // after o + (dp ? L : 0) - kStepSpan
     const bool far = l < nwin && !lit && db + span <= carry &&
-                     db + kRing < o + (dp ? L : 0u) + 260u;
+                     db + kRing < o + (dp ? L : 0u) + kStepSpan;
     if (!wave_ballot(litc || far))
         return fc;
     const uint32_t sdw = litc ? ipos >> 2 : db >> 2;           // first source dword
@@ -1082,6 +1234,16 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     }
     if (threadIdx.x < kWave)
         S.flags[threadIdx.x] = 0;             // chunk tags start at 0x80000001
+    for (uint32_t d = threadIdx.x; d < 2 * 16 * 8; d += 2 * kWave) {
+        const uint32_t h = d >> 7, p = (d >> 3) & 15, i0 = (d & 7) * 4;
+        uint32_t v = 0;
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint32_t idx = p ? (i0 + i) % p : 0u;
+            const uint32_t sel = h ? (idx >= 8 ? idx - 8 : 12u) : (idx < 8 ? idx : 12u);
+            v |= sel << (8 * i);
+        }
+        S.psel[h][p][d & 7] = v;
+    }
     __syncthreads();
 
     uint64_t acc[PH_N] = {};
@@ -1101,31 +1263,6 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     if (wave == 1) {
         if (POM_PRIO && last_round)
             __builtin_amdgcn_s_setprio(POM_PARSER_PRIO);
-#ifdef POM_EXPERIMENT_REPLAY
-        // (timing experiment only: publish the recorded pieces at once, then
-        // only the writer duty runs)
-        if (!refuse) {
-            const uint32_t* rec = (const uint32_t*)(gops + (kSlots - 1) * kOpMax);
-            uint32_t nq = 0;
-            for (; nq < kSlots - 1; nq++) {
-                const uint32_t info = rec[nq];
-                S.pinfo[nq] = info;
-                if (info & (kInfoEof | kInfoErr))
-                    break;
-            }
-            wave_order();
-            lds_store(&S.parsed, nq + 1);
-            WState w;
-            w.issued = 0;
-            w.landed = 0;
-            for (uint32_t spin = 0; spin < (1u << 22); spin++) {
-                if (writer_duty(S, k.out, l, w) != 0)
-                    break;
-                __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
-            }
-        }
-        return;
-#endif
         if (!refuse)
             parser_wave<STAMPS>(S, k, gops, l, acc);
         if (STAMPS && l == 0)
@@ -1136,9 +1273,12 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     }
 
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t base = lds_off(&S);
+    const uint32_t psel0 = lds_off(&S.psel[0][0][0]), psel1 = lds_off(&S.psel[1][0][0]);
     uint32_t carry = 0;                        // output produced so far
     uint32_t issued_seen = 0, landed_seen = 0; // last `issued` / `landed` read
     uint32_t tag = 0;                          // step counter for the chunk tags
+    uint32_t published = 0;                    // last `produced` handed to the writer
     uint32_t q = 0, w0 = 0, total_ops = 0;     // piece, window start, piece's op count
     bool have_piece = false, eofq = false;
     uint64_t pf = 0;                           // prefetched op record of the next window
@@ -1148,12 +1288,12 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         if (!have_piece) {
             // ---- the parser's piece q -------------------------------------------
             for (uint32_t spin = 0; lds_load(&S.parsed) <= q; spin++) {
-                if (spin > (1u << 22)) {       // parser stuck: let the exact path redo it
+                if (spin > (1u << 20)) {       // parser stuck: let the exact path redo it
                     refuse = true;
                     reason = RS_EWAIT;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(POM_EXEC_SLEEP);
             }
             if (refuse)
                 break;
@@ -1167,8 +1307,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             eofq = (info & kInfoEof) != 0;
             total_ops = info & 0xFFFFu;
 #ifdef POM_EXEC_SKIP
-            if (POM_EXEC_SKIP)                 // (timing experiment only: parser alone)
-                total_ops = 0;
+            total_ops = 0;                     // (measurement only: the parser alone)
 #endif
             have_piece = true;
             w0 = 0;
@@ -1178,7 +1317,6 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             lds_store(&S.consumed, q + 1);
             if (eofq)
                 break;                         // EOF consumed
-
             q++;
             have_piece = false;
             continue;
@@ -1288,25 +1426,14 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             uint32_t inv = 0;                          // mod by mulhi; only overlapping matches
             if (wave_ballot(dp != 0))
                 inv = dp ? 0xFFFFFFFFu / dp : 0u;
-            // An op needs HBM reads if its linear source is the input in HBM, or
-            // its output source may leave the ring before its last step
-            // (sp + kRing < step start + 260 for some byte; far ops the buffer
-            // did not take).
-            const bool gop = l < nwin && (outsrc ? db + kRing < o + (dp ? L : 0u) + 260u
-                                                 : (db & ~kLitFlag) + span > kLinHbm);
-            // Chunks: op j covers output chunks cs .. cs + ceil(L/4) - 1 of the
-            // window, each up to 4 bytes of that op alone.
-            const uint32_t nch = l < nwin ? (L + 3u) >> 2 : 0u;
+            // Chunks: op j covers the window's 16-byte chunks cs .. cs +
+            // ceil(L/16) - 1, each up to 16 bytes of that op alone.
+            const uint32_t nch = l < nwin ? (L + 15u) >> 4 : 0u;
             const uint32_t cinc = wave_incl_scan(nch);
             const uint32_t cs = cinc - nch;
             const uint32_t wchunks = lane_read(cinc, kWave - 1);
-            S.wop[l] = make_uint4(o, db, cs, L | (gop ? kLitFlag : 0u));
+            S.wop[l] = make_uint4(o, db, cs, L);
             S.wper[l] = make_uint2(dp, inv);
-            // 16-byte steps take a batch whose ops all read a contiguous
-            // source (no self-overlap) or repeat one byte (period 1), none of
-            // it from HBM.  The ring rule of `gop` covers them: it bounds a
-            // source by the op's start and end, not by the step length.
-            const bool wide_ok = !gop && dp <= 1u;
             wave_order();
             STAMP(PH_FARC);
             uint32_t s = 0;
@@ -1317,136 +1444,11 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nwin;
                 const uint32_t c_beg = lane_read(cs, s);
                 const uint32_t c_end = e < nwin ? lane_read(cs, e) : wchunks;
-                const bool gbatch = wave_ballot(l >= s && l < e && gop) != 0;
                 const bool starter = l >= s && l < e;
                 STAMP(PH_BATCH);
                 if (STAMPS)
                     acc[CN_BATCHES] += 1;
-                if (STAMPS) {
-                    const bool wb = !wave_ballot(starter && !wide_ok);
-                    acc[CN_WBATCHES] += wb;
-                    acc[CN_NW_GOP] += !wb && wave_ballot(starter && gop);
-                    acc[CN_NW_PER] += !wb && !wave_ballot(starter && gop);
-                }
-                if (POM_WIDE && !wave_ballot(starter && !wide_ok)) {
-                    // ---- batch [s, e) in 16-byte chunks, 64 per step (1 KiB) --
-                    // Same chunk -> op mapping as below; each op's first
-                    // 16-byte chunk replaces its 4-byte one in wop.z (an op
-                    // belongs to one batch only).
-                    const uint32_t n16 = starter ? (L + 15u) >> 4 : 0u;
-                    const uint32_t inc16 = wave_incl_scan(n16);
-                    const uint32_t cs16 = inc16 - n16;
-                    const uint32_t end16 = lane_read(inc16, kWave - 1);
-                    if (starter)
-                        S.wop[l].z = cs16;
-                    const uint32_t base = lds_off(&S);
-                    uint32_t jc = s;
-                    for (uint32_t C = 0; C < end16; C += kWave) {
-                        tag++;
-                        const uint32_t tagv = tag | 0x80000000u;
-                        if (starter && cs16 >= C && cs16 < C + kWave)
-                            S.flags[cs16 - C] = tagv;
-                        wave_order();
-                        const bool st0 = S.flags[l] == tagv;
-                        const uint64_t M = wave_ballot(st0);
-                        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
-                        const uint32_t j = (jc + below + (st0 ? 0u : ~0u)) & 63u;
-                        jc += (uint32_t)__builtin_popcountll(M);
-                        const uint4 op = S.wop[j];
-                        const uint32_t p1 = S.wper[j].x;          // 0 or 1
-                        const uint32_t c = C + l;
-                        const bool live = c < end16;
-                        const uint32_t k16 = (c - op.z) * 16u;
-                        const uint32_t x = op.x + k16;
-                        const uint32_t rem = op.w - k16;          // (no kLitFlag: !gop)
-                        const uint32_t len = live ? (rem < 16u ? rem : 16u) : 0u;
-                        const uint32_t nl = end16 - C < (uint32_t)kWave ? end16 - C : (uint32_t)kWave;
-                        const uint32_t xs = lane_read(x, 0);
-                        const uint32_t step_end = lane_read(x + len, nl - 1);
-                        for (uint32_t spin = 0; step_end > issued_seen + kRing; spin++) {
-                            if (spin > (1u << 22)) {
-                                refuse = true;
-                                reason = RS_SPACE;
-                                break;
-                            }
-                            if (spin)
-                                __builtin_amdgcn_s_sleep(1);
-                            issued_seen = lds_load(&S.issued);
-                        }
-                        if (refuse)
-                            break;
-                        if (STAMPS)
-                            acc[CN_STEPS] += 1;
-                        (void)xs;
-                        // source: 16 contiguous bytes, or the one repeated byte
-                        const bool lin = (op.y & kLitFlag) != 0;
-                        const uint32_t sa = (op.y & ~kLitFlag) + (p1 ? 0u : k16);
-                        const uint32_t ra = !live ? 0u : lin ? (sa & kLdsMask) : (sa & kRingMask);
-                        const uint32_t need = p1 ? 1u : len;
-                        const bool rcross = live && !lin && ra + need > kRing;
-                        uint4 v = lds_read16(base + ra);
-                        if (wave_ballot(rcross)) {
-                            if (rcross) {                      // source wraps the ring end
-                                const uint8_t* lds = (const uint8_t*)&S;
-                                uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-                                for (uint32_t i = 0; i < 16; i++)
-                                    w[i >> 2] |= (uint32_t)lds[(sa + i) & kRingMask] << (8 * (i & 3));
-                                v = make_uint4(w[0], w[1], w[2], w[3]);
-                            }
-                        }
-                        if (p1) {
-                            const uint32_t b4 = (v.x & 0xFFu) * 0x01010101u;
-                            v = make_uint4(b4, b4, b4, b4);
-                        }
-                        // destination: the ring at x
-                        const uint32_t xd = x & kRingMask;
-                        const bool wcross = live && xd + len > kRing;
-                        if (live && !wcross) {
-                            const uint32_t da = base + xd;
-                            if (len == 16u) {
-                                lds_write16(da, v);
-                            } else {
-                                uint32_t w0 = v.x, w1 = v.y, ad = da;
-                                if (len & 8u) {
-                                    lds_write8(ad, v.x, v.y);
-                                    w0 = v.z;
-                                    w1 = v.w;
-                                    ad += 8;
-                                }
-                                if (len & 4u) {
-                                    lds_write4(ad, w0);
-                                    w0 = w1;
-                                    ad += 4;
-                                }
-                                if (len & 2u) {
-                                    lds_write2(ad, w0);
-                                    w0 >>= 16;
-                                    ad += 2;
-                                }
-                                if (len & 1u)
-                                    lds_write1(ad, w0);
-                            }
-                        }
-                        if (wave_ballot(wcross)) {
-                            if (wcross) {                      // destination wraps the ring end
-                                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                                for (uint32_t i = 0; i < 16; i++)
-                                    if (i < len)
-                                        lds_write1(base + ((x + i) & kRingMask), w[i >> 2] >> (8 * (i & 3)));
-                            }
-                        }
-                        wave_order();
-                        lds_store(&S.produced, step_end);
-                    }
-                    if (refuse)
-                        break;
-                    s = e;
-                    continue;
-                }
-                // ---- batch [s, e): chunks [c_beg, c_end), 64 per step --------
+                // ---- batch [s, e): chunks [c_beg, c_end), 64 per step (1 KiB) ----
                 uint32_t jcarry = s;                   // ops of the batch started before C
                 for (uint32_t C = c_beg; C < c_end; C += kWave) {
                     // chunk -> op: each op starting in this step tags its first
@@ -1458,20 +1460,19 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         S.flags[cs - C] = tagv;
                     wave_order();
                     const bool st0 = S.flags[l] == tagv;
-                    const uint64_t M = wave_ballot(st0);
-                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+                    const uint64_t Mb = wave_ballot(st0);
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(Mb >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)Mb, 0u));
                     const uint32_t j = (jcarry + below + (st0 ? 0u : ~0u)) & 63u;
-                    jcarry += (uint32_t)__builtin_popcountll(M);
+                    jcarry += (uint32_t)__builtin_popcountll(Mb);
                     const uint4 op = S.wop[j];
                     const uint2 pr = S.wper[j];
                     const uint32_t c = C + l;
                     const bool live = c < c_end;
-                    const uint32_t k4 = (c - op.z) * 4u;
-                    const uint32_t x = op.x + k4;
-                    const uint32_t Lj = op.w & ~kLitFlag;
-                    const uint32_t rem = Lj - k4;
-                    const uint32_t len = live ? (rem < 4u ? rem : 4u) : 0u;
+                    const uint32_t k16 = (c - op.z) * 16u;
+                    const uint32_t x = op.x + k16;
+                    const uint32_t rem = op.w - k16;
+                    const uint32_t len = live ? (rem < 16u ? rem : 16u) : 0u;
                     const uint32_t nl = c_end - C < (uint32_t)kWave ? c_end - C : (uint32_t)kWave;
                     const uint32_t xs = lane_read(x, 0);
                     const uint32_t step_end = lane_read(x + len, nl - 1);
@@ -1479,13 +1480,18 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     // ring space: the stores of what the slots of [xs, step_end)
                     // held must have been issued
                     for (uint32_t spin = 0; step_end > issued_seen + kRing; spin++) {
-                        if (spin > (1u << 22)) {       // writer stuck: let the exact path redo it
+                        if (spin > (1u << 20)) {       // writer stuck: let the exact path redo it
                             refuse = true;
                             reason = RS_SPACE;
                             break;
                         }
-                        if (spin)
-                            __builtin_amdgcn_s_sleep(1);
+                        if (spin) {
+                            if (spin == 1) {           // hand over what is final
+                                lds_store(&S.produced, xs);
+                                published = xs;
+                            }
+                            __builtin_amdgcn_s_sleep(POM_EXEC_SLEEP);
+                        }
                         issued_seen = lds_load(&S.issued);
                     }
                     if (refuse)
@@ -1493,63 +1499,104 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     STAMP(PH_SPACE);
                     if (STAMPS)
                         acc[CN_STEPS] += 1;
-                    {
-                        // source offsets r_i = (k4 + i) mod p (p == 0: k4 + i)
-                        const uint32_t p = pr.x;
-                        uint32_t r[4];
-                        r[0] = k4 - p * (uint32_t)__umulhi(k4, pr.y);
-                        r[0] = min(r[0], r[0] - p);
-#pragma unroll
-                        for (uint32_t i = 1; i < 4; i++)
-                            r[i] = min(r[i - 1] + 1u, r[i - 1] + 1u - p);
-                        const bool lin = (op.y & kLitFlag) != 0;
-                        const uint32_t bb = live ? op.y & ~kLitFlag : 0u;
-                        // (linear sources in HBM read below; masking keeps their
-                        // LDS read inside the allocation)
-                        const uint32_t amask = !live ? 0u : lin ? kLdsMask : kRingMask;
-                        const uint8_t* lds = (const uint8_t*)&S;
-                        uint32_t val = 0;
-#pragma unroll
-                        for (uint32_t i = 0; i < 4; i++)
-                            val |= (uint32_t)lds[(bb + r[i]) & amask] << (8 * i);
-                        if (gbatch) {                          // literal in HBM / far match
-                            const bool gj = (op.w & kLitFlag) != 0;
-                            uint32_t gmask = 0;
-#pragma unroll
-                            for (uint32_t i = 0; i < 4; i++) {
-                                const uint32_t sp = bb + r[i];
-                                const bool isg = gj && i < len && (lin ? sp >= kLinHbm : sp + kRing < xs + 260u);
-                                gmask |= isg ? (1u << i) : 0u;
-                            }
-                            if (wave_ballot(gmask != 0)) {
-                                // output below xs + 260 - kRing is read from HBM
-                                if (xs + 260u > kRing)
-                                    landed_seen = wait_landed(S, xs + 260u - kRing, landed_seen, refuse);
-                                for (uint32_t i = 0; i < 4; i++) {
-                                    if (!(gmask & (1u << i)))
-                                        continue;
-                                    const uint32_t sp = bb + r[i];
-                                    const uint32_t bv = lin
-                                        ? (uint32_t)*((__attribute__((address_space(1))) const uint8_t*)(k.in + (sp - kLinHbm)))
-                                        : global_byte_nt(k.out + sp);
-                                    val = (val & ~(0xFFu << (8 * i))) | (bv << (8 * i));
-                                }
-                            }
+                    // ---- source bytes of the chunk ---------------------------
+                    // byte i reads src[b + ((k16 + i) mod p)] (p == 0: b + k16 + i)
+                    const uint32_t p = pr.x;
+                    const bool lin = (op.y & kLitFlag) != 0;
+                    const uint32_t bb = op.y & ~kLitFlag;
+                    uint32_t r0 = k16;
+                    if (p) {
+                        r0 = k16 - p * (uint32_t)__umulhi(k16, pr.y);
+                        r0 = min(r0, r0 - p);
+                    }
+                    const bool small = p != 0 && p < 16u;       // pattern expansion
+                    const uint32_t n1 = p - r0;                 // (p >= 16) bytes before the wrap
+                    const bool two = p >= 16u && n1 < len;      // the chunk wraps the period
+                    const uint32_t aA = small ? bb : bb + r0;
+                    const uint32_t aB = bb + r0 - p;            // wrapped part, read p lower
+                    const uint64_t smask = wave_ballot(live && small);
+                    const uint32_t ps = small ? p * 32u + r0 : 0u;   // selectors of the expansion
+                    // LDS: the ring (its mirror takes reads across the end) or
+                    // the linear source buffer; HBM: literals beyond the buffer,
+                    // output below the ring (a + kRing < xs: those slots were
+                    // overwritten before this step)
+                    const bool hA = live && (lin ? aA >= kLinHbm : aA + kRing < xs);
+                    const bool hB = live && two && (lin ? aB >= kLinHbm : bb + kRing < xs);
+                    const uint32_t amask = lin ? kLdsMask : kRingMask;
+                    uint4 vA, vB, sl, sh;
+                    lds_read16x4(base + (live ? aA & amask : 0u), base + (two ? aB & amask : 0u),
+                                 psel0 + ps, psel1 + ps, vA, vB, sl, sh);
+                    if (wave_ballot(hA || hB)) {
+                        if (wave_ballot((hA || hB) && !lin) && xs + 16u > kRing)
+                            landed_seen = wait_landed(S, xs + 16u - kRing, landed_seen, refuse);
+                        const uint8_t* gb = lin ? k.in - kLinHbm : k.out;
+                        if (hA)
+                            vA = global_read16(gb + aA, 0u, small ? p : two ? n1 : len);
+                        if (hB)                        // bytes n1.. of the span: from b on
+                            vB = global_read16(gb + bb - n1, n1, len);
+                    }
+                    if (refuse)
+                        break;
+                    uint4 v = vA;
+                    if (wave_ballot(two)) {
+                        // bytes i < n1 from vA, the rest from vB
+                        const uint32_t n = two ? n1 : 16u;
+                        const uint32_t m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1u;
+                        const uint32_t m1 = n >= 8 ? ~0u : n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1u;
+                        const uint32_t m2 = n >= 12 ? ~0u : n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1u;
+                        const uint32_t m3 = n >= 16 ? ~0u : n <= 12 ? 0u : (1u << (8 * (n - 12))) - 1u;
+                        v.x = (vA.x & m0) | (vB.x & ~m0);
+                        v.y = (vA.y & m1) | (vB.y & ~m1);
+                        v.z = (vA.z & m2) | (vB.z & ~m2);
+                        v.w = (vA.w & m3) | (vB.w & ~m3);
+                    }
+                    if (smask) {
+                        if (small) {
+                            v.x = __builtin_amdgcn_perm(vA.y, vA.x, sl.x) | __builtin_amdgcn_perm(vA.w, vA.z, sh.x);
+                            v.y = __builtin_amdgcn_perm(vA.y, vA.x, sl.y) | __builtin_amdgcn_perm(vA.w, vA.z, sh.y);
+                            v.z = __builtin_amdgcn_perm(vA.y, vA.x, sl.z) | __builtin_amdgcn_perm(vA.w, vA.z, sh.z);
+                            v.w = __builtin_amdgcn_perm(vA.y, vA.x, sl.w) | __builtin_amdgcn_perm(vA.w, vA.z, sh.w);
                         }
-                        uint8_t* ldsw = (uint8_t*)&S;
+                    }
+                    // ---- destination: the ring at x -----------------------------
+                    const uint32_t xd = x & kRingMask;
+                    const bool wcross = live && xd + len > kRing;
+                    if (live && !wcross) {
+                        lds_write_part(base + xd, v, len);
+                        if (xd < 16u)                  // keep the mirror of ring[0, 16)
+                            lds_write_part(base + kRing + xd, v, len);
+                    }
+                    if (wave_ballot(wcross)) {
+                        if (wcross) {                  // destination wraps the ring end
+                            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+                            uint8_t* ldsw = (uint8_t*)&S;
 #pragma unroll
-                        for (uint32_t i = 0; i < 4; i++)
-                            ldsw[i < len ? ((x + i) & kRingMask) : kSinkOff + i] = (uint8_t)(val >> (8 * i));
+                            for (uint32_t i = 0; i < 16; i++)
+                                if (i < len) {
+                                    const uint32_t y = (x + i) & kRingMask;
+                                    const uint8_t bv = (uint8_t)(wv[i >> 2] >> (8 * (i & 3)));
+                                    ldsw[y] = bv;
+                                    if (y < 16u)
+                                        ldsw[kRing + y] = bv;
+                                }
+                        }
                     }
                     wave_order();
                     STAMP(PH_GATHER);
-                    lds_store(&S.produced, step_end);  // bytes below are final: hand them over
+                    // bytes below step_end are final: hand them over once a
+                    // 1-KiB store chunk is complete (the writer stores whole chunks)
+                    if (!POM_LAZY_PUB || (step_end ^ published) >= kChunk) {
+                        lds_store(&S.produced, step_end);
+                        published = step_end;
+                    }
                     STAMP(PH_PUB);
                 }
                 if (refuse)
                     break;
                 s = e;
             }
+            if (refuse)
+                break;
             carry += wtotal;
             if (POM_PRIO && last_round)
                 prio_by_bytes_left(k.cap > carry ? k.cap - carry : 0u);
@@ -1568,6 +1615,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         if (refuse) {
             lds_store(&S.state, 2u);
             status[b] = kFallback;
+            out_len[b] = 0xFA110000u | reason;         // (diagnostics; the exact decoder rewrites it)
             const uint32_t at = atomicAdd(&fallback[0], 1u);
             fallback[1 + at] = b;
         } else {

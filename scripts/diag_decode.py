@@ -12,6 +12,7 @@ ap.add_argument("--blocks", type=int, default=4096)
 ap.add_argument("--model", default="itb")
 ap.add_argument("--bytes", type=int, default=65536)
 ap.add_argument("--lib", default=None, help="alternative liblzo_mi355x.so build")
+ap.add_argument("--nostamps", action="store_true", help="timing only (no stamps build run)")
 a = ap.parse_args()
 if a.lib:
     lzo.LIB_PATH = a.lib
@@ -50,7 +51,7 @@ def run(stamp):
         fn(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), p(opsbuf), nb, p(stamps), sh)
     else:
         fast(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), p(opsbuf), nb, sh)
-for stamp in (False, True):
+for stamp in ((False,) if a.nostamps else (False, True)):
     run(stamp); torch.cuda.synchronize()
     ts = []
     for _ in range(1 if stamp else 10):
@@ -59,6 +60,17 @@ for stamp in (False, True):
         ts.append(e0.elapsed_time(e1))
     print(f"stamps={stamp}: kernel {float(np.median(ts)):.3f} ms (median of {len(ts)}, min {min(ts):.3f}), "
           f"fallback {int(fb[0].item())}, equal {torch.equal(out, src.arena)}")
+    if not stamp and int(fb[0].item()):
+        olr = ol.cpu().numpy().astype(np.uint32)
+        fbb = np.nonzero((olr >> 16) == 0xFA11)[0]
+        print("  fast-path refusals (block, reason):", [(int(x), int(olr[x] & 15)) for x in fbb[:8]])
+        per = opsbuf.numel() // nb
+        for x in fbb[:4]:
+            blk = opsbuf[int(x) * per: (int(x) + 1) * per].cpu().numpy()
+            zs_ = za[int(zb.off[int(x)].item()): int(zb.off[int(x)].item()) + int(zl[int(x)].item())].cpu().numpy()
+            np.savez(os.path.join(ROOT, "gpurun_out", f"dead_b{int(x)}.npz"), ops=blk, z=zs_)
+if a.nostamps:
+    sys.exit(0)
 st = stamps.view(nb, SLOTS).double().cpu().numpy()
 # order of the kernel's PH_* / CN_* enum (lzo1x_decode_fast.hip)
 phases = ["stage", "pass1", "pwalk", "merge", "count", "write", "p_slotwait", "p_duty",

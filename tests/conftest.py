@@ -93,6 +93,16 @@ def malformed():
 
 
 @pytest.fixture(scope="session")
+def unchecked():
+    """The reference's UNCHECKED lzo1x_decompress on valid, trailing-byte,
+    concatenated and EOF-cut streams (tests/golden/make_golden.py)."""
+    z = np.load(os.path.join(GOLDEN, "unchecked.npz"))
+    return {"kinds": [str(k) for k in z["kind"]], "streams": _unpack(z["s_data"], z["s_off"]),
+            "rc": [int(r) for r in z["rc"]], "out_len": [int(n) for n in z["out_len"]],
+            "sha": [str(h) for h in z["out_sha256"]]}
+
+
+@pytest.fixture(scope="session")
 def manifest():
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         return json.load(f)["batches"]

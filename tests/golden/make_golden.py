@@ -13,6 +13,13 @@ repository).  Every vector below is the reference's own output:
                  past their end, the oracle's convention
   manifest.json  large batches (configs C1-C4): per-block compressed lengths
                  and SHA-256 of the concatenated compressed stream and input
+  unchecked.npz  the UNCHECKED lzo1x_decompress (the decoder Pomegranate calls,
+                 lib/minilzo.c:3308-3699) on valid streams, streams with
+                 trailing bytes, concatenated streams (the api/api.c:6666-6680
+                 fwritev layout read back by :6438) and streams whose EOF
+                 marker is cut short: return code (:3676-3680), *out_len and
+                 the SHA-256 of the produced bytes; inputs zero padded past
+                 their end
 
 Run:  make -C oracle && python tests/golden/make_golden.py
 """
@@ -59,6 +66,15 @@ class Ref:
         rc = self.lib.lzo1x_1_compress(src, n, out, ctypes.byref(olen), self.wrk)
         assert rc == 0
         return out.raw[: olen.value]
+
+    def decompress_unchecked(self, comp: bytes, out_cap: int):
+        """lzo1x_decompress (no bounds checks): the input is zero padded and the
+        output buffer oversized, so every case below stays in bounds."""
+        src = ctypes.create_string_buffer(comp + b"\0" * 4096, len(comp) + 4096)
+        out = ctypes.create_string_buffer(out_cap + 65536)
+        olen = _ulong(0xDEADBEEF)                  # ignored on input (:3326-3328)
+        rc = self.lib.lzo1x_decompress(src, len(comp), out, ctypes.byref(olen), None)
+        return rc, out.raw[: olen.value]
 
     def decompress_safe(self, comp: bytes, cap: int):
         src = ctypes.create_string_buffer(comp + b"\0" * PAD, len(comp) + PAD)
@@ -163,6 +179,42 @@ def malformed_cases(ref: Ref):
     return {int(k): rcs.count(k) for k in set(rcs)}
 
 
+def unchecked_cases(ref: Ref):
+    rng = random.Random(3699)
+    kinds, streams, rcs, olens, digests = [], [], [], [], []
+    for i in range(300):
+        mode = i % 6
+        n = rng.randrange(0, 6000) if i % 5 else rng.randrange(0, 300)
+        d = synth.block(i % 6, 12000 + i, n)
+        c = ref.compress(d)
+        if mode == 0:       # valid: LZO_E_OK
+            s, kind = c, "valid"
+        elif mode == 1:     # trailing bytes after EOF: INPUT_NOT_CONSUMED
+            s, kind = c + bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 9))), "trailing"
+        elif mode in (2, 3):  # per-iovec streams back to back (api/api.c:6666-6680)
+            parts = [c]
+            for k in range(mode):
+                m = rng.randrange(0, 2000)
+                parts.append(ref.compress(synth.block((i + k) % 6, 13000 + 7 * i + k, m)))
+            s, kind = b"".join(parts), f"concat{mode}"
+        elif mode == 4:     # EOF marker cut short: INPUT_OVERRUN (reads the zero pad)
+            s, kind = c[: len(c) - rng.choice((1, 2))], "eof_cut"
+        else:               # the EOF marker alone (an empty block) plus trailing bytes
+            s = c if n else c + bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 4)))
+            kind = "short"
+        rc, out = ref.decompress_unchecked(s, 4 * 6000)
+        kinds.append(kind)
+        streams.append(s)
+        rcs.append(rc)
+        olens.append(len(out))
+        digests.append(hashlib.sha256(out).hexdigest())
+    sd, so = pack(streams)
+    np.savez_compressed(os.path.join(OUT, "unchecked.npz"), kind=np.array(kinds), s_data=sd,
+                        s_off=so, rc=np.array(rcs, np.int32), out_len=np.array(olens, np.int64),
+                        out_sha256=np.array(digests))
+    return {int(k): rcs.count(k) for k in set(rcs)}
+
+
 def batch_entry(ref: Ref, name, model, seed0, sizes, note):
     arena, offs, lens = synth.batch(model, seed0, sizes)
     hz, hi = hashlib.sha256(), hashlib.sha256()
@@ -206,6 +258,7 @@ def main():
     ref = Ref()
     print("edge vectors:", edge_cases(ref))
     print("malformed rc histogram:", malformed_cases(ref))
+    print("unchecked rc histogram:", unchecked_cases(ref))
     print("manifest:", manifest(ref))
 
 

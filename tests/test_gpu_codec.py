@@ -124,6 +124,22 @@ def test_single_call_api(dev, edge):
     assert rc == 0 and got == bytes([0x11, 0, 0])
 
 
+def test_unchecked_decompress_codes(dev, unchecked):
+    """The unchecked lzo1x_decompress of the drop-in (what mds/itb.c:2964,
+    mdsl/gc.c:770 and api/api.c:6438 call) against the reference's own
+    unchecked decoder: return code, *out_len and bytes on valid streams,
+    trailing bytes, concatenated per-iovec streams and EOF-cut streams
+    (lib/minilzo.c:3676-3680)."""
+    bad = []
+    for i, (k, s, rc, n, sha) in enumerate(zip(unchecked["kinds"], unchecked["streams"],
+                                               unchecked["rc"], unchecked["out_len"],
+                                               unchecked["sha"])):
+        got_rc, got = lzo.lzo1x_decompress(s)
+        if (got_rc, len(got), hashlib.sha256(got).hexdigest()) != (rc, n, sha):
+            bad.append((i, k, got_rc, rc, len(got), n))
+    assert not bad, bad[:8]
+
+
 def test_host_batch_api(dev, edge, malformed):
     rc, st, comps = lzo.compress_batch(edge["inputs"][:300])
     assert rc == 0 and all(s == 0 for s in st)
