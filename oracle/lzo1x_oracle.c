@@ -241,7 +241,16 @@ struct dstate {
     uint8_t *out;
     size_t cap;
     size_t ip, op;
+    int unchecked;      /* lzo1x_decompress (no input checks) instead of _safe */
 };
+
+/* The unchecked decoder (lib/minilzo.c:3308-3699, LZO_TEST_OVERRUN undefined,
+ * :3214) reads past the input end without looking; with the input zero padded
+ * (the convention of every harness here) a stream that has not ended by then
+ * would read zeros forever, so a walk more than this many bytes past the end
+ * stops with INPUT_OVERRUN (the code :3676-3680 gives for ip > ip_end).
+ * The GPU exact decoder uses the same bound (lzo1x_kernels.hip). */
+#define ORC_UNCHECKED_SLACK 64
 
 static inline uint32_t rd(const struct dstate *s, size_t i)
 {
@@ -253,7 +262,16 @@ static inline uint32_t rd(const struct dstate *s, size_t i)
  * end the check passes (lib/minilzo.c:3733-3734). */
 static inline int need_ip(const struct dstate *s, size_t x)
 {
+    if (s->unchecked)
+        return s->ip <= s->in_len + ORC_UNCHECKED_SLACK;
     return !(s->ip <= s->in_len && s->in_len - s->ip < x);
+}
+
+/* TEST_IP at the top of the instruction loop (:3367, :3667): the safe decoder
+ * stops with EOF_NOT_FOUND at the input end; the unchecked one reads on. */
+static inline int test_ip(const struct dstate *s)
+{
+    return s->unchecked ? 1 : s->ip < s->in_len;
 }
 
 static inline int need_op(const struct dstate *s, size_t x)
@@ -294,10 +312,10 @@ static inline int read_ext(struct dstate *s, size_t base, size_t *t)
     return 1;
 }
 
-int oracle_lzo1x_decompress_safe(const uint8_t *in, size_t in_len,
-                                 uint8_t *out, size_t *out_len)
+static int decompress(const uint8_t *in, size_t in_len, uint8_t *out, size_t *out_len,
+                      int unchecked)
 {
-    struct dstate s = { in, in_len, out, *out_len, 0, 0 };
+    struct dstate s = { in, in_len, out, *out_len, 0, 0, unchecked };
     size_t t, dist;
     /* where: 0 = top of the instruction loop, 1 = right after a literal run,
      * 2 = a match opcode t is pending, 3 = trailing literals pending */
@@ -322,8 +340,10 @@ int oracle_lzo1x_decompress_safe(const uint8_t *in, size_t in_len,
 
     for (;;) {
         if (where == 0) {                  /* :3367-3414 */
-            if (!(s.ip < s.in_len))
+            if (!test_ip(&s))
                 goto no_eof;
+            if (!need_ip(&s, 1))
+                goto in_over;
             t = rd(&s, s.ip++);
             if (t >= 16) {
                 where = 2;
@@ -391,7 +411,7 @@ int oracle_lzo1x_decompress_safe(const uint8_t *in, size_t in_len,
         if (!need_ip(&s, t + 1)) goto in_over;
         copy_lits(&s, t);
         t = rd(&s, s.ip++);
-        if (!(s.ip < s.in_len))
+        if (!test_ip(&s))
             goto no_eof;
         where = 2;
     }
@@ -414,6 +434,25 @@ lb_over:
 fin:
     *out_len = s.op;
     return rc;
+}
+
+/* lzo1x_decompress_safe (lib/minilzo.c:3703-4190): *out_len is the capacity
+ * in, the produced length out. */
+int oracle_lzo1x_decompress_safe(const uint8_t *in, size_t in_len,
+                                 uint8_t *out, size_t *out_len)
+{
+    return decompress(in, in_len, out, out_len, 0);
+}
+
+/* lzo1x_decompress, the unchecked decoder Pomegranate calls (mds/itb.c:2964,
+ * mdsl/gc.c:770, api/api.c:6438): no input checks, so trailing bytes and
+ * back-to-back streams give INPUT_NOT_CONSUMED after the first EOF and a
+ * stream whose EOF marker is cut short INPUT_OVERRUN (:3676-3680).  *out_len
+ * is the output room in (the reference has none: the caller sizes it). */
+int oracle_lzo1x_decompress_unchecked(const uint8_t *in, size_t in_len,
+                                      uint8_t *out, size_t *out_len)
+{
+    return decompress(in, in_len, out, out_len, 1);
 }
 
 /* Worst-case compressed size used by every harness (lib/minilzo.h notes

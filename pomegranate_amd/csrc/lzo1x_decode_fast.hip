@@ -77,7 +77,7 @@ static_assert(kOpMax < (1u << 16), "piece info: 16-bit op count");
 constexpr uint32_t kSlots = POM_SLOTS;           // parsed pieces the parser may run ahead
 static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_WRITER_SLEEP
-#define POM_WRITER_SLEEP 32                      // idle writer sleeps ~2K cycles between polls
+#define POM_WRITER_SLEEP 127                     // idle writer sleeps ~8K cycles between polls
 #endif
 #ifndef POM_FWD_ROUNDS
 #define POM_FWD_ROUNDS 3                         // source-forwarding rounds per window
@@ -101,7 +101,7 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #define POM_LAZY_PUB 1                           // hand output to the writer per completed 1-KiB chunk
 #endif
 #ifndef POM_EXEC_SLEEP
-#define POM_EXEC_SLEEP 4                         // executor waits sleep ~256 cycles between polls
+#define POM_EXEC_SLEEP 16                        // executor waits sleep ~1K cycles between polls
 #endif
 #ifndef POM_DUTY_EVERY
 #define POM_DUTY_EVERY 4                         // parser pass-1 iterations between writer duties
@@ -492,6 +492,31 @@ __device__ __forceinline__ void lds_read16x4(uint32_t a, uint32_t b, uint32_t c,
     vb = make_uint4(y.x, y.y, y.z, y.w);
     vc = make_uint4(z.x, z.y, z.z, z.w);
     vd = make_uint4(w.x, w.y, w.z, w.w);
+}
+__device__ __forceinline__ uint4 lds_read16(uint32_t a)
+{
+    v4u32 x;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(a) : "memory");
+    return make_uint4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void lds_read16x2(uint32_t a, uint32_t b, uint4& va, uint4& vb)
+{
+    v4u32 x, y;
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(x), "=&v"(y) : "v"(a), "v"(b) : "memory");
+    va = make_uint4(x.x, x.y, x.z, x.w);
+    vb = make_uint4(y.x, y.y, y.z, y.w);
+}
+__device__ __forceinline__ void lds_read16x3(uint32_t a, uint32_t b, uint32_t c, uint4& va, uint4& vb,
+                                             uint4& vc)
+{
+    v4u32 x, y, z;
+    asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %4\n\tds_read_b128 %2, %5\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(x), "=&v"(y), "=&v"(z) : "v"(a), "v"(b), "v"(c) : "memory");
+    va = make_uint4(x.x, x.y, x.z, x.w);
+    vb = make_uint4(y.x, y.y, y.z, y.w);
+    vc = make_uint4(z.x, z.y, z.z, z.w);
 }
 __device__ __forceinline__ void lds_write16(uint32_t a, uint4 v)
 {
@@ -1523,9 +1548,21 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     const bool hA = live && (lin ? aA >= kLinHbm : aA + kRing < xs);
                     const bool hB = live && two && (lin ? aB >= kLinHbm : bb + kRing < xs);
                     const uint32_t amask = lin ? kLdsMask : kRingMask;
-                    uint4 vA, vB, sl, sh;
-                    lds_read16x4(base + (live ? aA & amask : 0u), base + (two ? aB & amask : 0u),
-                                 psel0 + ps, psel1 + ps, vA, vB, sl, sh);
+                    // only the reads some lane of the step needs (uniform branches)
+                    uint4 vA, vB = make_uint4(0, 0, 0, 0), sl = vB, sh = vB;
+                    const bool any_two = wave_ballot(two) != 0;
+                    const uint32_t ra = base + (live ? aA & amask : 0u);
+                    if (!smask) {
+                        if (!any_two)
+                            vA = lds_read16(ra);
+                        else
+                            lds_read16x2(ra, base + (two ? aB & amask : 0u), vA, vB);
+                    } else if (!any_two) {
+                        lds_read16x3(ra, psel0 + ps, psel1 + ps, vA, sl, sh);
+                    } else {
+                        lds_read16x4(ra, base + (two ? aB & amask : 0u), psel0 + ps, psel1 + ps, vA, vB, sl,
+                                     sh);
+                    }
                     if (wave_ballot(hA || hB)) {
                         if (wave_ballot((hA || hB) && !lin) && xs + 16u > kRing)
                             landed_seen = wait_landed(S, xs + 16u - kRing, landed_seen, refuse);
@@ -1538,7 +1575,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     if (refuse)
                         break;
                     uint4 v = vA;
-                    if (wave_ballot(two)) {
+                    if (any_two) {
                         // bytes i < n1 from vA, the rest from vB
                         const uint32_t n = two ? n1 : 16u;
                         const uint32_t m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1u;

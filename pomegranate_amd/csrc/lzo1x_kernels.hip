@@ -86,14 +86,21 @@ __device__ __forceinline__ uint32_t win_byte(InWin& W, uint32_t i)
 
 // ---------------------------------------------------------------------------
 // Exact decoder.  Mirrors the grammar walk of lib/minilzo.c:3308-3699 under
-// the safe decoder's checks (:3703-3761); WRITE=false is the length pre-scan
-// used by the unchecked single-call API (capacity unknown to the callee).
+// the safe decoder's checks (:3703-3761), or, with `unchecked`, the unchecked
+// lzo1x_decompress Pomegranate calls (LZO_TEST_OVERRUN undefined, :3214): no
+// input checks, so bytes past the end read as 0 (the fixtures' zero padding)
+// and only :3676-3680's three codes come out; a walk that runs more than
+// kUncheckedSlack bytes past the input end (where the reference would read
+// unrelated memory) stops with INPUT_OVERRUN, as oracle/lzo1x_oracle.c does.
+// WRITE=false is the length pre-scan used by the unchecked single-call API
+// (capacity unknown to the callee).
 // Output goes through a 64 KiB LDS ring (LZO1X looks back at most 0xBFFF
 // bytes, lib/minilzo.c:2653) and is flushed to HBM in 8 KiB pieces.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRing = 65536;
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kFlushQ = 8192;
+constexpr uint32_t kUncheckedSlack = 64;
 
 template <bool WRITE>
 struct Dec {
@@ -102,6 +109,7 @@ struct Dec {
     uint8_t* out;
     uint32_t cap;
     uint32_t ip, op, flushed;
+    bool unchecked;
 };
 
 template <bool WRITE>
@@ -183,6 +191,8 @@ template <bool WRITE>
 __device__ __forceinline__ bool dec_need_ip(const Dec<WRITE>& d, uint32_t x)
 {
     // lib/minilzo.c:3733-3734: (lzo_uint)(ip_end - ip) < x; passes once ip > ip_end
+    if (d.unchecked)
+        return d.ip <= d.W.len + kUncheckedSlack;
     return !(d.ip <= d.W.len && d.W.len - d.ip < x);
 }
 
@@ -231,8 +241,10 @@ __device__ int dec_run(Dec<WRITE>& d)
 
     for (;;) {
         if (where == 0) {                           // :3367-3414
-            if (!(d.ip < d.W.len))
+            if (!d.unchecked && !(d.ip < d.W.len))
                 return E_EOF_NOT_FOUND;
+            if (!dec_need_ip(d, 1))
+                return E_INPUT_OVERRUN;
             t = win_byte(d.W, d.ip++);
             if (t >= 16) {
                 where = 2;
@@ -304,7 +316,7 @@ __device__ int dec_run(Dec<WRITE>& d)
         if (!dec_need_ip(d, t + 1)) return E_INPUT_OVERRUN;
         dec_lits(d, t);
         t = win_byte(d.W, d.ip++);
-        if (!(d.ip < d.W.len))
+        if (!d.unchecked && !(d.ip < d.W.len))
             return E_EOF_NOT_FOUND;
         where = 2;
     }
@@ -316,7 +328,8 @@ __device__ void decode_exact_block(const uint8_t* __restrict__ src, const uint64
                                    const uint64_t* __restrict__ dst_off,
                                    const uint32_t* __restrict__ dst_cap,
                                    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-                                   uint8_t* ring, uint32_t b)
+                                   uint8_t* ring, uint32_t b, bool unchecked, uint32_t cap_limit,
+                                   uint32_t* __restrict__ cap_out)
 {
     Dec<WRITE> d;
     d.W.in = src + src_off[b];
@@ -327,11 +340,14 @@ __device__ void decode_exact_block(const uint8_t* __restrict__ src, const uint64
     d.out = dst ? dst + dst_off[b] : nullptr;
     d.cap = dst_cap ? dst_cap[b] : 0xFFFFFFFFu;
     d.ip = d.op = d.flushed = 0;
+    d.unchecked = unchecked;
     const int rc = dec_run(d);
     dec_flush(d, d.op);
     if (lane_id() == 0) {
         out_len[b] = d.op;
         status[b] = rc;
+        if (cap_out)                                // (pre-scan: the decode's capacity)
+            cap_out[b] = d.op < cap_limit ? d.op : cap_limit;
     }
 }
 
@@ -343,13 +359,14 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-    const uint32_t* __restrict__ fb, uint32_t nblocks)
+    const uint32_t* __restrict__ fb, uint32_t nblocks, bool unchecked, uint32_t cap_limit,
+    uint32_t* __restrict__ cap_out)
 {
     __shared__ uint8_t ring[WRITE ? kRing : 4];
     if (!fb) {
         if (blockIdx.x < nblocks)
             decode_exact_block<WRITE>(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                      status, ring, blockIdx.x);
+                                      status, ring, blockIdx.x, unchecked, cap_limit, cap_out);
         return;
     }
     const uint32_t count = fb[0];
@@ -357,7 +374,7 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
         const uint32_t b = fb[1 + i];
         if (b < nblocks)
             decode_exact_block<WRITE>(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                      status, ring, b);
+                                      status, ring, b, unchecked, cap_limit, cap_out);
     }
 }
 
@@ -586,25 +603,28 @@ extern "C" int lzo_mi355x_launch_decompress_exact(const uint8_t* src, const uint
                                                   const uint64_t* dst_off, const uint32_t* dst_cap,
                                                   uint32_t* out_len, int32_t* status,
                                                   const uint32_t* fb, uint32_t ngrid,
-                                                  uint32_t nblocks, hipStream_t stream)
+                                                  uint32_t nblocks, int unchecked,
+                                                  hipStream_t stream)
 {
     if (ngrid == 0)
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_exact_kernel<true>, dim3(ngrid), dim3(kWave), 0, stream, src,
-                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fb, nblocks);
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fb, nblocks,
+                       unchecked != 0, 0xFFFFFFFFu, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int lzo_mi355x_launch_decoded_length(const uint8_t* src, const uint64_t* src_off,
                                                 const uint32_t* src_len, uint32_t* out_len,
                                                 int32_t* status, uint32_t nblocks,
+                                                uint32_t* cap_out, uint32_t cap_limit,
                                                 hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_exact_kernel<false>, dim3(nblocks), dim3(kWave), 0, stream,
                        src, src_off, src_len, nullptr, nullptr, nullptr, out_len, status,
-                       nullptr, nblocks);
+                       nullptr, nblocks, true, cap_limit, cap_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -172,19 +172,20 @@ size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
 
 /* Fast decoder over the whole batch, then the exact decoder over the blocks
  * it refused (malformed input, capacity/lookbehind errors, pathological
- * streams).  Without scratch every block takes the exact decoder. */
-int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
-                              const uint32_t *src_len, uint8_t *dst,
-                              const uint64_t *dst_off, const uint32_t *dst_cap,
-                              uint32_t *out_len, int32_t *status, uint32_t nblocks,
-                              void *scratch, void *stream)
+ * streams).  Without scratch every block takes the exact decoder.
+ * unchecked: the exact decoder follows the unchecked lzo1x_decompress (the
+ * fast decoder only ever finishes streams on which both agree). */
+static int decompress_dev(const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                          uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
+                          uint32_t *out_len, int32_t *status, uint32_t nblocks, void *scratch,
+                          int unchecked, hipStream_t s)
 {
-    hipStream_t s = (hipStream_t)stream;
     if (nblocks == 0)
         return 0;
     if (!scratch)
         return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
-                                                  out_len, status, NULL, nblocks, nblocks, s);
+                                                  out_len, status, NULL, nblocks, nblocks,
+                                                  unchecked, s);
     uint32_t *fb = (uint32_t *)scratch;
     if (hipMemsetAsync(fb, 0, 4, s) != hipSuccess)
         return -1;
@@ -194,15 +195,25 @@ int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
         return -1;
     const uint32_t ngrid = nblocks < 512 ? nblocks : 512;
     return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
-                                              out_len, status, fb, ngrid, nblocks, s);
+                                              out_len, status, fb, ngrid, nblocks, unchecked, s);
+}
+
+int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
+                              const uint32_t *src_len, uint8_t *dst,
+                              const uint64_t *dst_off, const uint32_t *dst_cap,
+                              uint32_t *out_len, int32_t *status, uint32_t nblocks,
+                              void *scratch, void *stream)
+{
+    return decompress_dev(src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
+                          scratch, 0, (hipStream_t)stream);
 }
 
 int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,
                                   const uint32_t *src_len, uint32_t *out_len,
                                   int32_t *status, uint32_t nblocks, void *stream)
 {
-    return lzo_mi355x_launch_decoded_length(src, src_off, src_len, out_len, status, nblocks,
-                                            (hipStream_t)stream);
+    return lzo_mi355x_launch_decoded_length(src, src_off, src_len, out_len, status, nblocks, NULL,
+                                            0xFFFFFFFFu, (hipStream_t)stream);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -384,7 +395,7 @@ static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
     if (kind == OP_COMPRESS)
         rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, s);
     else
-        rc = lzo_mi355x_decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, s);
+        rc = decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, 0, s);
     if (rc != 0)
         return -1;
     if (hipMemcpyAsync(h + L->o_outlen, d + L->o_outlen, 8 * L->nb, hipMemcpyDeviceToHost, s) !=
@@ -538,98 +549,160 @@ unsigned lzo_version(void) { return LZO_VERSION; }
 const char *lzo_version_string(void) { return LZO_VERSION_STRING; }
 const char *lzo_version_date(void) { return LZO_VERSION_DATE; }
 
+/* ---- single calls ------------------------------------------------------------
+ * One block, one stream synchronisation: the header and the input go up, the
+ * kernels run, and the header plus an output region the host sizes up front
+ * come back in one go.  Staging (device and pinned host alike):
+ *   [0, 256)        header: src_off u64, dst_off u64, src_len, dst_cap,
+ *                   out_len, status, pre-scan length / status / capacity,
+ *                   fallback list (2 words)
+ *   [256, +G)       output (G: worst case, the caller's capacity, or a guess)
+ *   then the input, then the fast decoder's scratch (device only)
+ */
+enum { SC_HDR = 256 };
+struct sc_hdr {
+    uint64_t src_off, dst_off;
+    uint32_t src_len, dst_cap, out_len;
+    int32_t status;
+    uint32_t plen;
+    int32_t pstatus;
+    uint32_t pcap;
+    uint32_t fb[2];
+};
+
+enum sc_kind { SC_COMPRESS, SC_SAFE, SC_UNCHECKED };
+
+static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, uint8_t *dst,
+                       size_t room, size_t *produced)
+{
+    struct tctx *t = tctx_get();
+    if (!t || src_len > 0xFFFFFFF0u || room > 0xFFFFFFF0u)
+        return LZO_E_ERROR;
+    const size_t o_src = SC_HDR + ALIGN_UP(room, 256);
+    const size_t o_scr = o_src + ALIGN_UP(src_len, 256);
+    const size_t dneed = o_scr + (kind == SC_COMPRESS ? 0 : lzo_mi355x_decompress_scratch(1));
+    if (tctx_reserve(t, dneed, o_scr) != 0)
+        return LZO_E_ERROR;
+    uint8_t *h = t->hmem, *d = t->dmem;
+    hipStream_t s = t->stream;
+    struct sc_hdr *hh = (struct sc_hdr *)h;
+    memset(hh, 0, sizeof(*hh));
+    hh->src_off = o_src;
+    hh->dst_off = SC_HDR;
+    hh->src_len = (uint32_t)src_len;
+    hh->dst_cap = (uint32_t)room;
+    if (src_len)
+        memcpy(h + o_src, src, src_len);
+    struct sc_hdr *dh = (struct sc_hdr *)d;
+    const uint64_t *so = &dh->src_off, *dof = &dh->dst_off;
+    const uint32_t *sl = &dh->src_len;
+    if (hipMemcpyAsync(d, h, sizeof(*hh), hipMemcpyHostToDevice, s) != hipSuccess ||
+        (src_len && hipMemcpyAsync(d + o_src, h + o_src, src_len, hipMemcpyHostToDevice, s) !=
+                        hipSuccess))
+        return LZO_E_ERROR;
+    int rc = 0;
+    if (kind == SC_COMPRESS) {
+        rc = lzo_mi355x_compress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
+                                     s);
+    } else if (kind == SC_SAFE) {
+        rc = decompress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
+                            d + o_scr, 0, s);
+    } else {
+        /* the unchecked decoder's own length, capped at the room (decoded
+         * again with more room when it does not fit) */
+        rc = lzo_mi355x_launch_decoded_length(d, so, sl, &dh->plen, &dh->pstatus, 1, &dh->pcap,
+                                              (uint32_t)room, s);
+        if (rc == 0)
+            rc = decompress_dev(d, so, sl, d, dof, &dh->pcap, &dh->out_len, &dh->status, 1,
+                                d + o_scr, 1, s);
+    }
+    if (rc != 0 || hipMemcpyAsync(h, d, o_src, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return LZO_E_ERROR;
+    if (kind == SC_UNCHECKED && hh->plen > room) {
+        *produced = hh->plen;                      /* needs more room: the caller retries */
+        return 1;
+    }
+    const size_t n = hh->out_len < room ? hh->out_len : room;
+    if (n)
+        memcpy(dst, h + SC_HDR, n);
+    *produced = hh->out_len;
+    return hh->status;
+}
+
+/* lib/minilzo.c:3159-3207.  The output is the reference's with a zero-filled
+ * wrkmem (SURVEY.md finding 3), so wrkmem is not read. */
 int lzo1x_1_compress(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst, lzo_uintp dst_len,
                      lzo_voidp wrkmem)
 {
-    (void)wrkmem;   /* output is the zero-filled-wrkmem output by definition */
-    const uint8_t *s[1] = { src };
-    uint8_t *d[1] = { dst };
-    size_t sl[1] = { src_len }, dl[1] = { 0 };
-    int st[1] = { LZO_E_ERROR };
-    int rc = lzo_mi355x_compress_batch(s, sl, d, dl, st, 1);
-    if (rc != LZO_E_OK)
-        return rc;
-    *dst_len = dl[0];
-    return st[0];
+    (void)wrkmem;
+    size_t n = 0;
+    const int rc = single_call(SC_COMPRESS, src, src_len, dst,
+                               lzo_mi355x_worst_compress(src_len), &n);
+    if (rc != LZO_E_ERROR)
+        *dst_len = n;
+    return rc;
 }
 
+/* lib/minilzo.c:3703-4190: *dst_len is the capacity in, the produced length out. */
 int lzo1x_decompress_safe(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst,
                           lzo_uintp dst_len, lzo_voidp wrkmem)
 {
     (void)wrkmem;
-    const uint8_t *s[1] = { src };
-    uint8_t *d[1] = { dst };
-    size_t sl[1] = { src_len }, dl[1] = { *dst_len };
-    int st[1] = { LZO_E_ERROR };
-    int rc = lzo_mi355x_decompress_batch(s, sl, d, dl, st, 1);
-    if (rc != LZO_E_OK)
-        return rc;
-    *dst_len = dl[0];
-    return st[0];
+    size_t n = 0;
+    const int rc = single_call(SC_SAFE, src, src_len, dst, *dst_len, &n);
+    if (rc != LZO_E_ERROR)
+        *dst_len = n;
+    return rc;
 }
 
 /* GPU pre-scan of one host-resident stream: decoded length and status. */
-static int prescan_one(struct tctx *t, const uint8_t *src, size_t src_len, uint32_t *olen)
-{
-    const size_t meta = 256;
-    const size_t need = meta + ALIGN_UP(src_len, 16);
-    if (tctx_reserve(t, need, need) != 0)
-        return LZO_E_ERROR;
-    uint8_t *h = t->hmem, *d = t->dmem;
-    uint64_t zero = 0;
-    uint32_t len32 = (uint32_t)src_len;
-    memcpy(h, &zero, 8);
-    memcpy(h + 8, &len32, 4);
-    if (src_len)
-        memcpy(h + meta, src, src_len);
-    hipStream_t s = t->stream;
-    if (hipMemcpyAsync(d, h, need, hipMemcpyHostToDevice, s) != hipSuccess)
-        return LZO_E_ERROR;
-    if (lzo_mi355x_decoded_length_dev(d + meta, (const uint64_t *)d, (const uint32_t *)(d + 8),
-                                      (uint32_t *)(d + 16), (int32_t *)(d + 20), 1, s) != 0)
-        return LZO_E_ERROR;
-    if (hipMemcpyAsync(h + 16, d + 16, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return LZO_E_ERROR;
-    int32_t st;
-    memcpy(olen, h + 16, 4);
-    memcpy(&st, h + 20, 4);
-    return st;
-}
-
 int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len, unsigned long *dst_len)
 {
     struct tctx *t = tctx_get();
     if (!t || src_len > 0xFFFFFFF0u)
         return LZO_E_ERROR;
-    uint32_t olen = 0;
-    int st = prescan_one(t, src, src_len, &olen);
-    *dst_len = olen;
-    return st;
+    const size_t o_src = SC_HDR;
+    if (tctx_reserve(t, o_src + src_len + 16, o_src + src_len + 16) != 0)
+        return LZO_E_ERROR;
+    uint8_t *h = t->hmem, *d = t->dmem;
+    hipStream_t s = t->stream;
+    struct sc_hdr *hh = (struct sc_hdr *)h, *dh = (struct sc_hdr *)d;
+    memset(hh, 0, sizeof(*hh));
+    hh->src_off = o_src;
+    hh->src_len = (uint32_t)src_len;
+    if (src_len)
+        memcpy(h + o_src, src, src_len);
+    if (hipMemcpyAsync(d, h, o_src + src_len, hipMemcpyHostToDevice, s) != hipSuccess ||
+        lzo_mi355x_launch_decoded_length(d, &dh->src_off, &dh->src_len, &dh->plen, &dh->pstatus,
+                                         1, NULL, 0xFFFFFFFFu, s) != 0 ||
+        hipMemcpyAsync(h, d, sizeof(*hh), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return LZO_E_ERROR;
+    *dst_len = hh->plen;
+    return hh->pstatus;
 }
 
-/* The unchecked entry point never learns the destination size
- * (mds/itb.c:2951-2964 passes an uninitialised *out_len).  The decoded length
- * is computed on the GPU first, then the block is decoded into exactly that
- * many bytes. */
+/* The unchecked decoder (lib/minilzo.c:3308-3699) that mds/itb.c:2964,
+ * mdsl/gc.c:770 and api/api.c:6438 call.  It never learns the destination
+ * size (mds/itb.c:2951-2964 passes an uninitialised *out_len): the GPU
+ * pre-scans the stream's decoded length in the same launch sequence and the
+ * output comes back with it; only a block that decodes to more than the
+ * guessed room (16x the input, at least 256 KiB) takes a second round trip. */
 int lzo1x_decompress(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst, lzo_uintp dst_len,
                      lzo_voidp wrkmem)
 {
     (void)wrkmem;
-    struct tctx *t = tctx_get();
-    if (!t || src_len > 0xFFFFFFF0u)
-        return LZO_E_ERROR;
-    uint32_t olen = 0;
-    int st0 = prescan_one(t, src, src_len, &olen);
-    if (st0 == LZO_E_ERROR)
-        return LZO_E_ERROR;
-    const uint8_t *sp[1] = { src };
-    uint8_t *dp[1] = { dst };
-    size_t sl[1] = { src_len }, dl[1] = { olen };
-    int st[1] = { LZO_E_ERROR };
-    int rc = lzo_mi355x_decompress_batch(sp, sl, dp, dl, st, 1);
-    if (rc != LZO_E_OK)
-        return rc;
-    *dst_len = dl[0];
-    return st[0];
+    size_t room = (size_t)src_len * 16;
+    if (room < ((size_t)256 << 10))
+        room = (size_t)256 << 10;
+    if (room > 0xFFFFFFF0u)
+        room = 0xFFFFFFF0u;
+    size_t n = 0;
+    int rc = single_call(SC_UNCHECKED, src, src_len, dst, room, &n);
+    if (rc == 1)                                   /* longer than the guess */
+        rc = single_call(SC_UNCHECKED, src, src_len, dst, n, &n);
+    if (rc != LZO_E_ERROR)
+        *dst_len = n;
+    return rc;
 }

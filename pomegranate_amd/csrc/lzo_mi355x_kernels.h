@@ -30,15 +30,16 @@ int lzo_mi355x_launch_compress(const uint8_t *src, const uint64_t *src_off,
                                uint32_t *out_len, int32_t *status, uint32_t nblocks,
                                int pending_only, hipStream_t stream);
 
-/* Exact (grammar-serial) decoder, lzo1x_decompress_safe semantics.  fb NULL:
- * grid entry b decodes block b (ngrid = nblocks).  Otherwise the fb[0] blocks
- * listed at fb[1..] are decoded by a grid of ngrid workgroups. */
+/* Exact (grammar-serial) decoder, lzo1x_decompress_safe semantics, or with
+ * `unchecked` those of the unchecked lzo1x_decompress.  fb NULL: grid entry b
+ * decodes block b (ngrid = nblocks).  Otherwise the fb[0] blocks listed at
+ * fb[1..] are decoded by a grid of ngrid workgroups. */
 int lzo_mi355x_launch_decompress_exact(const uint8_t *src, const uint64_t *src_off,
                                        const uint32_t *src_len, uint8_t *dst,
                                        const uint64_t *dst_off, const uint32_t *dst_cap,
                                        uint32_t *out_len, int32_t *status,
                                        const uint32_t *fb, uint32_t ngrid,
-                                       uint32_t nblocks, hipStream_t stream);
+                                       uint32_t nblocks, int unchecked, hipStream_t stream);
 
 /* Throughput decoder (lzo1x_decode_fast.hip).  Blocks it does not finish
  * exactly are appended to fb (fb[0] = count, must be 0 on entry) and get
@@ -52,9 +53,12 @@ int lzo_mi355x_launch_decompress_fast(const uint8_t *src, const uint64_t *src_of
                                       uint32_t *out_len, int32_t *status, uint32_t *fb,
                                       void *ops, uint32_t nblocks, hipStream_t stream);
 
+/* Unchecked-decoder pre-scan: decoded length and status per block; with
+ * cap_out, also min(length, cap_limit) per block (a decode's capacity). */
 int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off,
                                      const uint32_t *src_len, uint32_t *out_len,
-                                     int32_t *status, uint32_t nblocks, hipStream_t stream);
+                                     int32_t *status, uint32_t nblocks, uint32_t *cap_out,
+                                     uint32_t cap_limit, hipStream_t stream);
 
 /* Host side (lzo_host.c), not part of the ABI: len[i] bytes from src[i] to
  * dst[i] for every i, split over up to 8 threads once the total is large. */

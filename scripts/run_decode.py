@@ -13,6 +13,7 @@ ap.add_argument("--bytes", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--model", default="itb")
 ap.add_argument("--lib", default=None, help="alternative liblzo_mi355x.so build")
+ap.add_argument("--noverify", action="store_true", help="exit 0 even if the output differs (timing variants)")
 a = ap.parse_args()
 if a.lib:
     lzo.LIB_PATH = a.lib
@@ -38,4 +39,4 @@ torch.cuda.synchronize()
 ok = torch.equal(out, src.arena) and bool((st == 0).all())
 print({"blocks": nb, "n_bytes": int(lens.astype(np.int64).sum()), "z_bytes": int(zl.long().sum()),
        "reps": a.reps, "ok": ok}, flush=True)
-sys.exit(0 if ok else 1)
+sys.exit(0 if ok or a.noverify else 1)

@@ -38,9 +38,9 @@ class Oracle:
         self.lib.oracle_lzo1x_1_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t,
                                                      ctypes.c_void_p,
                                                      ctypes.POINTER(ctypes.c_size_t)]
-        self.lib.oracle_lzo1x_decompress_safe.argtypes = [ctypes.c_void_p, ctypes.c_size_t,
-                                                          ctypes.c_void_p,
-                                                          ctypes.POINTER(ctypes.c_size_t)]
+        for fn in ("oracle_lzo1x_decompress_safe", "oracle_lzo1x_decompress_unchecked"):
+            getattr(self.lib, fn).argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                              ctypes.POINTER(ctypes.c_size_t)]
 
     def compress(self, data: bytes) -> bytes:
         n = len(data)
@@ -55,6 +55,14 @@ class Oracle:
         out = ctypes.create_string_buffer(max(cap, 1))
         ol = ctypes.c_size_t(cap)
         rc = self.lib.oracle_lzo1x_decompress_safe(src, len(comp), out, ctypes.byref(ol))
+        return rc, out.raw[: ol.value]
+
+    def decompress_unchecked(self, comp: bytes, room: int = 1 << 22):
+        """lzo1x_decompress semantics (no input checks; room = output buffer)."""
+        src = ctypes.create_string_buffer(comp, max(len(comp), 1))
+        out = ctypes.create_string_buffer(max(room, 1))
+        ol = ctypes.c_size_t(room)
+        rc = self.lib.oracle_lzo1x_decompress_unchecked(src, len(comp), out, ctypes.byref(ol))
         return rc, out.raw[: ol.value]
 
 

@@ -140,6 +140,16 @@ def test_unchecked_decompress_codes(dev, unchecked):
     assert not bad, bad[:8]
 
 
+@pytest.mark.parametrize("n", [65536, 262145, 536192, (2 << 20) + 7])
+def test_unchecked_single_call_large_output(dev, oracle, n):
+    """Outputs beyond the single call's first guess (16x the input, at least
+    256 KiB) take the second round trip; bytes and length stay exact."""
+    d = synth.block(synth.ITB, 31337 + n, n)
+    z = oracle.compress(d)
+    rc, back = lzo.lzo1x_decompress(z)
+    assert rc == 0 and back == d
+
+
 def test_host_batch_api(dev, edge, malformed):
     rc, st, comps = lzo.compress_batch(edge["inputs"][:300])
     assert rc == 0 and all(s == 0 for s in st)
