@@ -35,11 +35,15 @@ int lzo_mi355x_device_count(void);
  * at most dst_cap[b] bytes at dst + dst_off[b]; out_len[b] and status[b]
  * (LZO_E_* code) are written when the stream reaches the work.
  */
+/* `scratch`: device memory of lzo_mi355x_compress_scratch(nblocks) bytes for
+ * the per-workgroup match dictionaries (32 KiB each; 16 blocks per CU are then
+ * parsed at once), or NULL (dictionaries in LDS: 4 blocks per CU). */
 int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                             const uint32_t *src_len, uint8_t *dst,
                             const uint64_t *dst_off, const uint32_t *dst_cap,
                             uint32_t *out_len, int32_t *status, uint32_t nblocks,
-                            void *stream);
+                            void *scratch, void *stream);
+size_t lzo_mi355x_compress_scratch(uint32_t nblocks);
 
 /* Decompression with lzo1x_decompress_safe semantics per block (capacity
  * dst_cap[b]).  `scratch` is device memory of lzo_mi355x_decompress_scratch()

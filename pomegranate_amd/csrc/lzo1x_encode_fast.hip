@@ -67,10 +67,21 @@ constexpr uint32_t kFarPos = 0xC0000000u;        // a read position past every b
 #define POM_ENC_AHEAD 2048                      // bytes the emit wave pulls into L2 ahead of the parse
 #endif
 
-struct __attribute__((aligned(16))) EncLds {
+// The dictionary lives in LDS (4 blocks per CU: it is 32 KiB) or, with
+// scratch from the caller, in global memory: 32 KiB per resident workgroup,
+// so 16 blocks per CU parse at once (4 parse waves per SIMD instead of one)
+// at the price of a probe round trip through L2 instead of LDS.
+#ifndef POM_ENC_RESIDENT
+#define POM_ENC_RESIDENT 16                     // workgroups per CU with the global dictionary (2 waves each: the CU wave limit)
+#endif
+constexpr uint32_t kDictBytes = (kSlots + 2) * 2 + 60;   // per workgroup, 64-byte multiple
+static_assert(kDictBytes % 64 == 0, "dictionary regions stay 64-byte aligned");
+
+template <bool GD>
+struct __attribute__((aligned(16))) EncLdsT {
     // (each array has one spare entry past its end: the target of the writes
     // of lanes that take no part, instead of an exec-masked branch)
-    uint16_t dict[kSlots + 2];      // last probe position per hash slot: position - base + 1 (0 = empty)
+    uint16_t dict[GD ? 2 : kSlots + 2]; // last probe position per hash slot: position - base + 1 (0 = empty)
     uint32_t claim[kClaim + 1];     // (window tag << 8 | lowest writing lane) per hashed slot
     uint4 tok[kTok + 1];            // {literal start, literal count, match length (0: tail), offset}
     uint8_t stage[kStage];          // emitter output ring
@@ -79,8 +90,47 @@ struct __attribute__((aligned(16))) EncLds {
     uint32_t ip;                    // the parse wave's window start (a prefetch hint)
     uint32_t sink;                  // prefetched words end here
 };
-// four blocks (eight waves) per CU
-static_assert(sizeof(EncLds) * 4 <= 160 * 1024, "LDS budget");
+typedef EncLdsT<false> EncLds;
+// four blocks (eight waves) per CU; with the global dictionary, twelve
+static_assert(sizeof(EncLdsT<false>) * 4 <= 160 * 1024, "LDS budget");
+static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budget");
+
+// Dictionary access: S.dict (LDS) or the workgroup's region in global memory
+// (non-temporal loads: served by L2, so a load sees this wave's earlier
+// dictionary stores).
+typedef __attribute__((address_space(1))) uint16_t gu16;
+template <bool GD>
+struct Dict {
+    uint16_t* lds;
+    gu16* g;
+    __device__ __forceinline__ uint32_t get(uint32_t slot) const
+    {
+        if (GD)
+            return __builtin_nontemporal_load(g + slot);
+        return lds[slot];
+    }
+    __device__ __forceinline__ void put(uint32_t slot, uint32_t v) const
+    {
+        if (GD)
+            g[slot] = (uint16_t)v;
+        else
+            lds[slot] = (uint16_t)v;
+    }
+    // dwords 2i, 2i+1 of the table as one u32 (zeroing, re-basing)
+    __device__ __forceinline__ uint32_t get2(uint32_t i) const
+    {
+        if (GD)
+            return __builtin_nontemporal_load((__attribute__((address_space(1))) uint32_t*)g + i);
+        return ((uint32_t*)lds)[i];
+    }
+    __device__ __forceinline__ void put2(uint32_t i, uint32_t v) const
+    {
+        if (GD)
+            ((__attribute__((address_space(1))) uint32_t*)g)[i] = v;
+        else
+            ((uint32_t*)lds)[i] = v;
+    }
+};
 
 __device__ __forceinline__ uint32_t lane_id() { return emit::lane(); }
 __device__ __forceinline__ uint32_t claim_index(uint32_t slot) { return (slot ^ (slot >> 9)) & (kClaim - 1); }
@@ -206,8 +256,9 @@ enum { EP_SETUP, EP_PROBE, EP_CAND, EP_PATH, EP_CLAIM, EP_TOK, EP_DICT, EP_PUSHW
        EC_WINDOWS, EC_EXTEND, EC_TOKENS, EC_PATHIT, EC_EXTIT, EC_C2NEED, EC_C2MATCH, EC_FWD, EP_N };
 constexpr int kEncStampSlots = 16;
 
-template <bool STAMPS>
-__device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l, uint64_t* acc)
+template <bool STAMPS, bool GD>
+__device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, uint32_t n, uint32_t l,
+                           uint64_t* acc)
 {
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #define ESTAMP(ph)                                                  \
@@ -239,9 +290,11 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
     uint32_t ii = 0;                                // first byte not yet emitted
     if (n > 13) {                                   // lib/minilzo.c:3167-3173
         for (uint32_t s = l; s < kSlots / 2; s += kWave)
-            ((uint32_t*)S.dict)[s] = 0;             // zero-filled wrkmem: all EMPTY
+            D.put2(s, 0);                           // zero-filled wrkmem: all EMPTY
         for (uint32_t s = l; s < kClaim; s += kWave)
             S.claim[s] = 0xFFFFFFFFu;               // (tag 0xFFFFFF: no window has it)
+        if (GD)
+            __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0): the table is zero in L2
         wave_order();
         const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
         uint32_t ip = 4;
@@ -260,12 +313,14 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
                 const uint32_t nb = (ip - (kM4MaxOffset + 1)) / kRebase * kRebase;
                 const uint32_t delta = nb - base;
                 for (uint32_t s2 = l; s2 < kSlots / 2; s2 += kWave) {
-                    const uint32_t pr = ((uint32_t*)S.dict)[s2];
+                    const uint32_t pr = D.get2(s2);
                     const uint32_t lo = pr & 0xFFFFu, hi = pr >> 16;
                     const uint32_t nlo = lo > delta ? lo - delta : 0u;
                     const uint32_t nhi = hi > delta ? hi - delta : 0u;
-                    ((uint32_t*)S.dict)[s2] = nlo | (nhi << 16);
+                    D.put2(s2, nlo | (nhi << 16));
                 }
+                if (GD)
+                    __builtin_amdgcn_s_waitcnt(0x0F70);
                 wave_order();
                 base = nb;
             }
@@ -277,7 +332,7 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             const uint32_t h1 = emit::slot_primary(pw[0] & 0xFF, (pw[0] >> 8) & 0xFF,
                                                    (pw[0] >> 16) & 0xFF, pw[0] >> 24);
             const uint32_t h2 = emit::slot_secondary(h1);
-            const uint32_t e1 = S.dict[h1], e2 = S.dict[h2];
+            const uint32_t e1 = D.get(h1), e2 = D.get(h2);
             const uint32_t w1 = active && e1 ? base + e1 - 1 : 0u;   // (positions >= 4: 0 stays "empty")
             const uint32_t w2 = active && e2 ? base + e2 - 1 : 0u;
             const uint64_t am = wave_ballot(active);
@@ -465,7 +520,12 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
             }
             // UPDATE_I of every path lane before the cut but the superseded ones: their slots are distinct
             ESTAMP(EP_TOK);
-            S.dict[(path & keep & ~superseded) >> l & 1ull ? slot : kSlots] = (uint16_t)(p - base + 1);
+            if (GD) {
+                if ((path & keep & ~superseded) >> l & 1ull)
+                    D.put(slot, p - base + 1);
+            } else {
+                D.put((path & keep & ~superseded) >> l & 1ull ? slot : kSlots, p - base + 1);
+            }
             wave_order();
             ESTAMP(EP_DICT);
             if (done)
@@ -485,7 +545,8 @@ __device__ void parse_wave(EncLds& S, const uint8_t* in, uint32_t n, uint32_t l,
 // ---------------------------------------------------------------------------
 // Emit wave
 // ---------------------------------------------------------------------------
-__device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap,
+template <bool GD>
+__device__ void emit_wave(EncLdsT<GD>& S, const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap,
                           uint32_t* out_len, int32_t* status, uint32_t b)
 {
     emit::Enc e;
@@ -679,18 +740,19 @@ __device__ void emit_wave(EncLds& S, const uint8_t* in, uint32_t n, uint8_t* out
     }
 }
 
-template <bool STAMPS>
-__global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
-    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
-    uint64_t* __restrict__ stamps)
+// One block: both waves, then the workgroup is ready for the next one.
+template <bool STAMPS, bool GD>
+__device__ __forceinline__ void encode_block(EncLdsT<GD>& S, const Dict<GD> D,
+                                             const uint8_t* __restrict__ src,
+                                             const uint64_t* __restrict__ src_off,
+                                             const uint32_t* __restrict__ src_len,
+                                             uint8_t* __restrict__ dst,
+                                             const uint64_t* __restrict__ dst_off,
+                                             const uint32_t* __restrict__ dst_cap,
+                                             uint32_t* __restrict__ out_len,
+                                             int32_t* __restrict__ status, uint32_t b,
+                                             uint64_t* __restrict__ stamps)
 {
-    __shared__ EncLds S;
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks)
-        return;
     const uint32_t n = src_len[b];
     if (n > kMaxN) {                                 // (u32 positions, 16-bit token lengths kept small)
         if (threadIdx.x == 0)
@@ -708,27 +770,97 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
     const uint8_t* in = src + src_off[b];
     if (wave == 0) {
         uint64_t acc[EP_N] = {};
-        parse_wave<STAMPS>(S, in, n, l, acc);
+        parse_wave<STAMPS, GD>(S, D, in, n, l, acc);
         if (STAMPS && l == 0)
             for (int i = 0; i < EP_N; i++)
                 stamps[(size_t)b * kEncStampSlots + i] = acc[i];
     } else
-        emit_wave(S, in, n, dst + dst_off[b], dst_cap[b], out_len, status, b);
+        emit_wave<GD>(S, in, n, dst + dst_off[b], dst_cap[b], out_len, status, b);
+}
+
+template <bool STAMPS>
+__global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
+    uint64_t* __restrict__ stamps)
+{
+    __shared__ EncLds S;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    Dict<false> D;
+    D.lds = S.dict;
+    D.g = nullptr;
+    encode_block<STAMPS, false>(S, D, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
+                                b, stamps);
+}
+
+// Global-dictionary encoder: a grid of resident workgroups, each with its
+// own dictionary region, working through the blocks grid-stride.
+template <bool STAMPS>
+__global__ __launch_bounds__(2 * kWave, POM_ENC_RESIDENT / 2) void lzo1x_encode_gdict_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
+    uint8_t* __restrict__ dicts, uint64_t* __restrict__ stamps)
+{
+    __shared__ EncLdsT<true> S;
+    Dict<true> D;
+    D.lds = nullptr;
+    D.g = (gu16*)(dicts + (size_t)blockIdx.x * kDictBytes);
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        encode_block<STAMPS, true>(S, D, src, src_off, src_len, dst, dst_off, dst_cap, out_len,
+                                   status, b, stamps);
+        __syncthreads();                             // both waves done with the block
+    }
 }
 
 }  // namespace
+
+static uint32_t enc_resident(void)
+{
+    static int cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return 256 * POM_ENC_RESIDENT;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        cus[dev] = n;
+    }
+    return (uint32_t)cus[dev] * POM_ENC_RESIDENT;
+}
+
+extern "C" size_t lzo_mi355x_compress_scratch(uint32_t nblocks)
+{
+    const uint32_t g = nblocks < enc_resident() ? nblocks : enc_resident();
+    return (size_t)g * kDictBytes;
+}
 
 extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_t* src_off,
                                                const uint32_t* src_len, uint8_t* dst,
                                                const uint64_t* dst_off, const uint32_t* dst_cap,
                                                uint32_t* out_len, int32_t* status,
-                                               uint32_t nblocks, hipStream_t stream)
+                                               uint32_t nblocks, void* scratch, size_t scratch_bytes,
+                                               hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_encode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0, stream,
-                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
-                       nullptr);
+    uint32_t grid = scratch ? (uint32_t)(scratch_bytes / kDictBytes) : 0u;
+    grid = grid < nblocks ? grid : nblocks;
+    grid = grid < enc_resident() ? grid : enc_resident();
+    if (grid)
+        hipLaunchKernelGGL(lzo1x_encode_gdict_kernel<false>, dim3(grid), dim3(2 * kWave), 0, stream,
+                           src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
+                           (uint8_t*)scratch, nullptr);
+    else
+        hipLaunchKernelGGL(lzo1x_encode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0, stream,
+                           src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
+                           nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -144,7 +144,7 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                             const uint32_t *src_len, uint8_t *dst,
                             const uint64_t *dst_off, const uint32_t *dst_cap,
                             uint32_t *out_len, int32_t *status, uint32_t nblocks,
-                            void *stream)
+                            void *scratch, void *stream)
 {
     /* blocks up to 16 MiB: the throughput encoder; larger ones are left
      * pending for the general encoder, whose other workgroups exit at once */
@@ -152,7 +152,8 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
     if (nblocks == 0)
         return 0;
     if (lzo_mi355x_launch_compress_fast(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                        status, nblocks, s) != 0)
+                                        status, nblocks, scratch,
+                                        scratch ? lzo_mi355x_compress_scratch(nblocks) : 0, s) != 0)
         return -1;
     return lzo_mi355x_launch_compress(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
                                       status, nblocks, 1, s);
@@ -336,7 +337,9 @@ static void layout_make(struct layout *L, size_t nb, const size_t *src_len, cons
     L->o_dst = o;
     o += ALIGN_UP(d, 256);
     L->o_scr = o;
-    o += ALIGN_UP(lzo_mi355x_decompress_scratch((uint32_t)nb), 256);
+    const size_t scr_d = lzo_mi355x_decompress_scratch((uint32_t)nb);
+    const size_t scr_c = lzo_mi355x_compress_scratch((uint32_t)nb);
+    o += ALIGN_UP(scr_d > scr_c ? scr_d : scr_c, 256);
     L->total = o;
     L->o_pack = o;
     L->dtotal = o + ALIGN_UP(d, 256);
@@ -393,7 +396,7 @@ static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
     int32_t *st = (int32_t *)(d + L->o_status);
     int rc;
     if (kind == OP_COMPRESS)
-        rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, s);
+        rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, s);
     else
         rc = decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, 0, s);
     if (rc != 0)
@@ -603,7 +606,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
     int rc = 0;
     if (kind == SC_COMPRESS) {
         rc = lzo_mi355x_compress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
-                                     s);
+                                     NULL, s);   /* one block: the LDS dictionary is faster */
     } else if (kind == SC_SAFE) {
         rc = decompress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
                             d + o_scr, 0, s);

@@ -15,12 +15,14 @@ extern "C" {
 #define LZO_MI355X_ENC_PENDING 0x7FFF0002
 
 /* Throughput encoder (lzo1x_encode_fast.hip), blocks of up to 16 MiB; larger
- * blocks get status LZO_MI355X_ENC_PENDING. */
+ * blocks get status LZO_MI355X_ENC_PENDING.  With scratch (scratch_bytes of
+ * device memory, lzo_mi355x_compress_scratch()) the dictionaries live there
+ * and 16 blocks per CU are parsed at once; without, in LDS (4 per CU). */
 int lzo_mi355x_launch_compress_fast(const uint8_t *src, const uint64_t *src_off,
                                     const uint32_t *src_len, uint8_t *dst,
                                     const uint64_t *dst_off, const uint32_t *dst_cap,
                                     uint32_t *out_len, int32_t *status, uint32_t nblocks,
-                                    hipStream_t stream);
+                                    void *scratch, size_t scratch_bytes, hipStream_t stream);
 
 /* General encoder (lzo1x_kernels.hip), any block size below 32 MiB.
  * pending_only: only blocks whose status is LZO_MI355X_ENC_PENDING. */

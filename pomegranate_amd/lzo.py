@@ -44,6 +44,7 @@ EXPORTS = (
     "lzo_mi355x_worst_compress", "lzo_mi355x_device_count", "lzo_mi355x_decoded_length",
     "lzo_mi355x_compress_dev", "lzo_mi355x_decompress_dev",
     "lzo_mi355x_decompress_scratch", "lzo_mi355x_decoded_length_dev",
+    "lzo_mi355x_compress_scratch",
     "lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
     # include/pom_itb.h
     "pom_itb_lzo_compress_batch", "pom_itb_lzo_decompress_batch",
@@ -97,7 +98,9 @@ def load() -> ctypes.CDLL:
     lib.lzo_mi355x_device_count.restype = ctypes.c_int
     dev_args = [_u8p, _u8p, _u8p, _u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_uint32]
     lib.lzo_mi355x_compress_dev.restype = ctypes.c_int
-    lib.lzo_mi355x_compress_dev.argtypes = dev_args + [_u8p]
+    lib.lzo_mi355x_compress_dev.argtypes = dev_args + [_u8p, _u8p]
+    lib.lzo_mi355x_compress_scratch.restype = _size
+    lib.lzo_mi355x_compress_scratch.argtypes = [ctypes.c_uint32]
     lib.lzo_mi355x_decompress_dev.restype = ctypes.c_int
     lib.lzo_mi355x_decompress_dev.argtypes = dev_args + [_u8p, _u8p]
     lib.lzo_mi355x_decompress_scratch.restype = _size
@@ -225,14 +228,27 @@ def _stream_handle(torch, stream=None) -> int:
     return int(s.cuda_stream)
 
 
-def compress_dev(src: DeviceBatch, dst: DeviceBatch, out_len, status, stream=None) -> None:
-    """Enqueue LZO1X-1 compression of every block of src into dst (dst.length = capacity)."""
+def compress_dev(src: DeviceBatch, dst: DeviceBatch, out_len, status, scratch="auto",
+                 stream=None) -> None:
+    """Enqueue LZO1X-1 compression of every block of src into dst (dst.length = capacity).
+
+    scratch: device tensor of compress_scratch_bytes(nblocks) bytes for the
+    per-workgroup match dictionaries (16 blocks per CU parse at once), None for
+    LDS dictionaries (4 per CU), or "auto" to allocate one for this call."""
     import torch
+    if isinstance(scratch, str):
+        nbytes = compress_scratch_bytes(src.nblocks)
+        scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=src.arena.device)
     rc = load().lzo_mi355x_compress_dev(
         _ptr(src.arena), _ptr(src.off), _ptr(src.length), _ptr(dst.arena), _ptr(dst.off),
-        _ptr(dst.length), _ptr(out_len), _ptr(status), src.nblocks, _stream_handle(torch, stream))
+        _ptr(dst.length), _ptr(out_len), _ptr(status), src.nblocks,
+        _ptr(scratch) if scratch is not None else None, _stream_handle(torch, stream))
     if rc != 0:
         raise RuntimeError("lzo_mi355x_compress_dev launch failed")
+
+
+def compress_scratch_bytes(nblocks: int) -> int:
+    return int(load().lzo_mi355x_compress_scratch(nblocks))
 
 
 def decompress_dev(src: DeviceBatch, dst: DeviceBatch, out_len, status, scratch=None,

@@ -12,6 +12,7 @@ ap.add_argument("--blocks", type=int, default=4096)
 ap.add_argument("--model", default="itb")
 ap.add_argument("--bytes", type=int, default=65536)
 ap.add_argument("--lib", default=None)
+ap.add_argument("--nostamps", action="store_true")
 a = ap.parse_args()
 if a.lib:
     lzo.LIB_PATH = a.lib
@@ -35,19 +36,31 @@ if fn is not None:
     fn.argtypes = [ctypes.c_void_p] * 8 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 p = lambda x: x.data_ptr()
 sh = torch.cuda.current_stream().cuda_stream
-for stamp in ((False, True) if fn is not None else (False,)):
+scr = torch.empty(max(lzo.compress_scratch_bytes(nb), 1), dtype=torch.uint8, device=dev)
+ref_out = None
+for mode in ("lds", "gdict", "stamps"):
+    if mode == "stamps" and (fn is None or a.nostamps):
+        continue
     ts = []
-    for _ in range(1 if stamp else 5):
+    for _ in range(1 if mode == "stamps" else 5):
+        za.zero_()
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-        if stamp:
+        if mode == "stamps":
             fn(p(src.arena), p(src.off), p(src.length), p(za), p(zb.off), p(zb.length), p(zl), p(zs), nb, p(stamps), sh)
         else:
-            lzo.compress_dev(src, zb, zl, zs)
+            lzo.compress_dev(src, zb, zl, zs, scratch=scr if mode == "gdict" else None)
         e1.record(); torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
-    print(f"stamps={stamp}: {float(np.median(ts)):.3f} ms (min {min(ts):.3f}), status ok {bool((zs == 0).all())}")
-if fn is None:
+    same = ""
+    if mode != "stamps":
+        got = (za.clone(), zl.clone())
+        if ref_out is None:
+            ref_out = got
+        else:
+            same = f", identical to lds {torch.equal(got[0], ref_out[0]) and torch.equal(got[1], ref_out[1])}"
+    print(f"{mode}: {float(np.median(ts)):.3f} ms (min {min(ts):.3f}), status ok {bool((zs == 0).all())}{same}")
+if fn is None or a.nostamps:
     sys.exit(0)
 st = stamps.view(nb, SLOTS).double().cpu().numpy()
 phases = ["setup", "probe", "cand", "path", "claim", "tok", "dict", "pushwait"]
