@@ -1,24 +1,30 @@
 #!/usr/bin/env python3
 """LZO1X block codec benchmark on MI355X (BASELINE.json metric).
 
-Default workload (BASELINE.json configs[1], C2): 4096 x 64 KiB synthetic ITB
-blocks per GPU, LZO1X decompress-only, device-resident: inputs (the compressed
-blocks) and outputs live in HBM before the timed region starts.  A "step" is
-one decompression pass over the whole batch.  value = uncompressed GiB/s over
-all GPUs (sum of n over every rank / max-over-ranks time).
+The metric is "LZO1X compress+decompress GiB/s (device-resident)".  Default
+workload (BASELINE.json configs[2], C3): 4096 x 64 KiB synthetic ITB blocks
+per GPU in HBM before the timed region starts.  A "step" is one LZO1X-1
+compression of the whole batch followed by one decompression of what it just
+produced; value = uncompressed bytes of every rank / max-over-ranks wall time
+of the steps, in GiB/s (so value = n / (t_compress + t_decompress)).
 
-Also reported on the default line (not the headline): LZO1X-1 compress GiB/s
-and compress + decompress round-trip GiB/s on the same blocks (C3), the HBM
-roofline of the decode kernel, and the reference's own lib/minilzo.c
-(oracle/_ref, compiled from the reference sources) timed on this box's host
-cores on a bounded sample -- whose compressed bytes are also compared with the
-GPU's (C3 byte identity).
+Also on the line: the decode-only rate of the same batch (configs[1], C2,
+timed on its own), the HBM roofline of each kernel (`roofline` is the decoder,
+whose roofline fraction the north star targets; `compress_roofline` the
+encoder, the larger share of a step), and the reference's own lib/minilzo.c
+(oracle/_ref, compiled from the reference sources) on this box's host cores:
+a bounded sample of the same ITB blocks, whose compressed bytes are also
+compared with the GPU's (C3 byte identity), and configs[0] (C1: random 64
+KiB blocks, compress -> decompress round trip on the CPU).
 
 Other workloads (--workload):
+  c2  decompress-only steps (configs[1])
   c4  mixed 4-256 KiB ITB blocks, decompress GiB/s; --c4-blocks per GPU
       (default 131072 = 1 M / 8: the 8-GPU run is exactly configs[3])
   c5  end-to-end ITB write/read through the MDSL append-file loopback with
       the host-resident batch API (pinned staging, hipMemcpyAsync in and out)
+  single  per-call latency of the minilzo.h drop-in (lzo1x_1_compress,
+      lzo1x_decompress) at ITB sizes, next to lib/minilzo.c on the host
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): global
 block i goes to rank i mod N (weak scaling: per-GPU work fixed); the only
@@ -48,7 +54,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=("c2", "c4", "c5"), default="c2")
+    p.add_argument("--workload", choices=("c3", "c2", "c4", "c5", "single"), default="c3")
     p.add_argument("--blocks", type=int, default=4096, help="C2: blocks per GPU")
     p.add_argument("--block-bytes", type=int, default=65536)
     p.add_argument("--c4-blocks", type=int, default=131072, help="C4: blocks per GPU")
@@ -63,6 +69,83 @@ def parse():
 # ---------------------------------------------------------------------------
 # CPU baseline: the reference's lib/minilzo.c on the host cores
 # ---------------------------------------------------------------------------
+def host_cores():
+    """Host cores this process may run on: its CPU affinity set, capped by
+    OMP_NUM_THREADS when that is set (the GPU box sets it to the box's share
+    of a shared machine, 16 per GPU, and os.cpu_count() counts the whole
+    machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
+def _ref_lib():
+    """lib/minilzo.c compiled from the reference sources (oracle/_ref), or None."""
+    path = os.path.join(ROOT, "oracle", "_ref", "libminilzo_ref.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    for f in (lib.lzo1x_decompress, lib.lzo1x_1_compress):
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                      ctypes.POINTER(ctypes.c_ulong), ctypes.c_void_p]
+    getattr(lib, "__lzo_init_v2")(0x2040, 2, 4, 8, 4, 8, 8, 8, 8, 48)
+    return lib
+
+
+def cpu_c1(synth, seconds):
+    """configs[0] (C1): lib/minilzo.c compress -> decompress round trip of
+    random 64 KiB blocks (xorshift64, seed 42 + b) on the host cores, a
+    bounded sample (the full 1 K blocks take minutes at ~0.08 GiB/s/core)."""
+    from concurrent.futures import ThreadPoolExecutor
+    lib = _ref_lib()
+    if lib is None:
+        return None
+    threads = host_cores()
+    blocks = [synth.block(synth.RANDOM, 42 + b, 65536) for b in range(max(threads, 16))]
+    ulong = ctypes.c_ulong
+
+    def share(t, deadline, res):
+        wrk = ctypes.create_string_buffer(131072)
+        z = ctypes.create_string_buffer(65536 + 65536 // 16 + 128)
+        o = ctypes.create_string_buffer(65536 + 64)
+        tc = td = 0.0
+        done = 0
+        b = t
+        while time.perf_counter() < deadline:
+            src = blocks[b % len(blocks)]
+            zl, ol = ulong(0), ulong(0)
+            t0 = time.perf_counter()
+            ctypes.memset(wrk, 0, 131072)
+            lib.lzo1x_1_compress(src, len(src), z, ctypes.byref(zl), wrk)
+            t1 = time.perf_counter()
+            rc = lib.lzo1x_decompress(z, zl.value, o, ctypes.byref(ol), None)
+            t2 = time.perf_counter()
+            assert rc == 0 and ol.value == len(src) and o.raw[: ol.value] == src
+            tc += t1 - t0
+            td += t2 - t1
+            done += len(src)
+            b += threads
+        res[t] = (done, tc, td)
+
+    res = [None] * threads
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda t: share(t, t0 + seconds, res), range(threads)))
+    wall = time.perf_counter() - t0
+    n = sum(r[0] for r in res)
+    tc = sum(r[1] for r in res) / threads
+    td = sum(r[2] for r in res) / threads
+    return {"roundtrip_value": round(n / wall / GIB, 4), "unit": "GiB/s", "cores": threads,
+            "compress_value": round(n / threads / tc / GIB * threads, 4) if tc else None,
+            "decompress_value": round(n / threads / td / GIB * threads, 4) if td else None,
+            "kind": "reference",
+            "sample": f"configs[0]: random 64 KiB blocks (seed 42+b) compressed and decompressed "
+                      f"by lib/minilzo.c (oracle/_ref) on {threads} threads for {seconds:.0f} s "
+                      f"({int(n) >> 16} blocks)"}
 def cpu_baseline(plain, comps, seconds):
     """Reference lib/minilzo.c (oracle/_ref) or, if absent, the oracle port, on
     the host cores: decompress (and compress) of a bounded sample.  The
@@ -89,8 +172,7 @@ def cpu_baseline(plain, comps, seconds):
         kind = "port"
         dec = None
         comp = None
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16, os.cpu_count() or 1))
+    threads = host_cores()
     nsample = len(plain)
     lens = [len(p) for p in plain]
     srcs = [ctypes.create_string_buffer(comps[b], len(comps[b]) + 64) for b in range(nsample)]
@@ -157,19 +239,33 @@ def cpu_baseline(plain, comps, seconds):
                          if kind == "reference" else "oracle/lzo1x_oracle.c port")}
 
 
-def load_traffic(block_bytes, nblocks):
-    """HBM bytes per decode launch from the committed rocprofv3 PMC summary,
-    when one exists for this workload (profiles/*decode_pmc.json; the newest
-    file name wins)."""
+KERNEL_SOURCES = {"decode": "pomegranate_amd/csrc/lzo1x_decode_fast.hip",
+                  "encode": "pomegranate_amd/csrc/lzo1x_encode_fast.hip"}
+
+
+def source_sha16(kind):
+    """SHA-256 (16 hex digits) of the kernel's source file: the build a
+    profile summary was measured on."""
+    import hashlib
+    with open(os.path.join(ROOT, KERNEL_SOURCES[kind]), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def load_traffic(kind, block_bytes, nblocks):
+    """HBM bytes per launch of the decode / encode kernel from a committed
+    rocprofv3 PMC summary (profiles/*_{kind}_pmc.json, scripts/profile_pmc.py)
+    measured on THIS kernel source (its source_sha16 must match), else None."""
     import glob
+    sha = source_sha16(kind)
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*decode_pmc.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*{kind}_pmc.json"))):
         try:
             with open(path) as f:
                 j = json.load(f)
         except Exception:
             continue
-        if j.get("block_bytes") == block_bytes and j.get("nblocks") == nblocks:
+        if (j.get("block_bytes") == block_bytes and j.get("nblocks") == nblocks and
+                j.get("source_sha16") == sha):
             best = j
     return best
 
@@ -214,6 +310,8 @@ class Resident:
         self.ost = torch.zeros(nb, dtype=torch.int32, device=dev)
         nscr = lzo.decompress_scratch_bytes(nb)
         self.scratch = torch.empty(max(nscr, 1), dtype=torch.uint8, device=dev)
+        self.cscratch = torch.empty(max(lzo.compress_scratch_bytes(nb), 1), dtype=torch.uint8,
+                                    device=dev)
         self.compress()
         torch.cuda.synchronize()
         self.zsrc = lzo.DeviceBatch(zarena, self.zdst.off, self.zlen)
@@ -223,7 +321,7 @@ class Resident:
         self.fallback_blocks = int(self.scratch[:4].view(torch.int32).item())
 
     def compress(self):
-        self.lzo.compress_dev(self.src, self.zdst, self.zlen, self.zst)
+        self.lzo.compress_dev(self.src, self.zdst, self.zlen, self.zst, self.cscratch)
 
     def decompress(self):
         self.lzo.decompress_dev(self.zsrc, self.odst, self.olen, self.ost, self.scratch)
@@ -274,36 +372,59 @@ class Resident:
         return plain, comps
 
 
-def timed(torch, dist, world, stream, fn, steps, warmup):
-    """Wall time of `steps` calls (barrier + synchronize on both sides) and the
-    HIP-event time per call on the stream the kernels run on."""
+def timed(torch, dist, world, stream, phases, steps, warmup):
+    """Wall time of `steps` steps (each: the phases in order), bracketed by a
+    barrier and a synchronize on both sides, and the average HIP-event time of
+    each phase on the stream its kernels run on."""
     for _ in range(warmup):
-        fn()
+        for f in phases:
+            f()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
+           for _ in range(steps)]
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
-        fn()
-    ev1.record(stream)
+    for k in range(steps):
+        evs[k][0].record(stream)
+        for i, f in enumerate(phases):
+            f()
+            evs[k][i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    return wall, ev0.elapsed_time(ev1) / 1e3 / max(steps, 1)
+    per = [sum(evs[k][i].elapsed_time(evs[k][i + 1]) for k in range(steps)) / 1e3 / max(steps, 1)
+           for i in range(len(phases))]
+    return wall, per
+
+
+def roofline(kind, nbytes, kernel_s, block_bytes, nblocks, note):
+    """HBM roofline of one kernel: algorithmic bytes (compressed + uncompressed,
+    SURVEY.md §8(d)) per launch over the launch's average duration."""
+    achieved = nbytes / kernel_s / 1e9
+    rec = load_traffic(kind, block_bytes, nblocks)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
+            "traffic_source": rec.get("profile") if rec else None,
+            "kernel_ms": round(kernel_s * 1e3, 4), "algorithmic_bytes_per_launch": int(nbytes),
+            "kernel": note}
 
 
 def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend):
     model = {v: k for k, v in synth.MODEL_NAMES.items()}[args.model]
-    if args.workload == "c2":
+    if args.workload in ("c2", "c3"):
         nglobal = args.blocks * world
         mine = shard.round_robin(nglobal, rank, world)         # global ids i = rank mod G
         sizes = [args.block_bytes] * len(mine)
-        workload = (f"configs[1]: {args.blocks} x {args.block_bytes // 1024} KiB {args.model} "
-                    "blocks per GPU, LZO1X decompress-only, device-resident")
+        if args.workload == "c3":
+            workload = (f"configs[2]: {args.blocks} x {args.block_bytes // 1024} KiB {args.model} "
+                        "blocks per GPU, LZO1X-1 compress + decompress round trip, "
+                        "device-resident, byte identity vs lib/minilzo.c checked")
+        else:
+            workload = (f"configs[1]: {args.blocks} x {args.block_bytes // 1024} KiB {args.model} "
+                        "blocks per GPU, LZO1X decompress-only, device-resident")
     else:
         nglobal = args.c4_blocks * world
         mine = shard.round_robin(nglobal, rank, world)
@@ -313,72 +434,81 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
     R = Resident(torch, lzo, synth, dev, model, sizes, np.asarray(mine, dtype=np.uint64))
     stream = torch.cuda.current_stream()
     errors = R.errors()
-    dec_wall, dec_kernel = timed(torch, dist, world, stream, R.decompress, args.steps,
-                                 args.warmup)
-    comp_wall, comp_kernel = timed(torch, dist, world, stream, R.compress,
-                                   args.compress_steps, 1)
-    errors += int((R.ost != 0).sum().item()) + int((R.zst != 0).sum().item())
     n_bytes, z_bytes = R.n_bytes, R.z_bytes
+    bb = args.block_bytes if args.workload != "c4" else None
+    # headline: C3 steps (compress, then decompress what it produced), or
+    # decompress-only steps for c2 / c4
+    if args.workload == "c3":
+        wall, (t_c, t_d) = timed(torch, dist, world, stream, [R.compress, R.decompress],
+                                 args.steps, args.warmup)
+        errors += R.errors()                               # the last step's round trip
+        dec_wall, (t_d2,) = timed(torch, dist, world, stream, [R.decompress], args.steps, 1)
+    else:
+        wall, (t_d,) = timed(torch, dist, world, stream, [R.decompress], args.steps, args.warmup)
+        dec_wall, t_d2 = wall, t_d
+        _, (t_c,) = timed(torch, dist, world, stream, [R.compress], args.compress_steps, 1)
+        errors += int((R.ost != 0).sum().item()) + int((R.zst != 0).sum().item())
     if world > 1:
-        errors, dec_wall = shard.completion_barrier(dist, dev, errors, dec_wall)
-        _, comp_wall = shard.completion_barrier(dist, dev, 0, comp_wall)
+        errors, wall = shard.completion_barrier(dist, dev, errors, wall)
+        _, dec_wall = shard.completion_barrier(dist, dev, 0, dec_wall)
         tot = torch.tensor([n_bytes, z_bytes], dtype=torch.float64,
                            device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tot)
         n_all, z_all = float(tot[0].item()), float(tot[1].item())
     else:
         n_all, z_all = n_bytes, z_bytes
-
-    value = n_all * args.steps / dec_wall / GIB
-    comp_gibps = n_all * args.compress_steps / comp_wall / GIB
-    rt_gibps = n_all / (dec_wall / args.steps + comp_wall / args.compress_steps) / GIB
-    achieved = (z_bytes + n_bytes) / dec_kernel / 1e9          # per GPU, decode launch
-    traffic = None
-    if args.workload == "c2":
-        rec = load_traffic(args.block_bytes, args.blocks)
-        traffic = rec.get("hbm_bytes_per_launch") if rec else None
+    value = n_all * args.steps / wall / GIB
+    dec_gibps = n_all * args.steps / dec_wall / GIB
+    nb = len(mine)
+    if args.workload == "c3":
+        metric = METRIC
+    else:
+        metric = "LZO1X decompress GiB/s (device-resident), " + (
+            "4096 x 64 KiB ITB blocks" if args.workload == "c2" else "mixed 4-256 KiB ITB blocks")
     result = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dec_wall / args.steps * 1e3, 4),
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic ITB payload images (SURVEY.md Appendix B generator, libpom_synth)",
-        "config": {"workload": workload, "blocks_per_gpu": len(mine),
-                   "block_bytes": args.block_bytes if args.workload == "c2" else "4-256 KiB",
+        "config": {"workload": workload, "blocks_per_gpu": nb,
+                   "block_bytes": args.block_bytes if args.workload != "c4" else "4-256 KiB",
                    "compression_ratio": round(z_all / n_all, 4),
                    "parallelism": f"round-robin blocks over {world} GPU(s)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic,
-                     "kernel_ms": round(dec_kernel * 1e3, 4),
-                     "algorithmic_bytes_per_launch": int(z_bytes + n_bytes)},
-        "compress_gibps": round(comp_gibps, 3),
-        "roundtrip_gibps": round(rt_gibps, 3),
-        "compress_kernel_ms": round(comp_kernel * 1e3, 3),
+        # the decoder's roofline (the north star's target); the encoder's next to it
+        "roofline": roofline("decode", z_bytes + n_bytes, t_d, bb, nb,
+                             "lzo1x_decode_fast_kernel (+ the exact pass over its refusals)"),
+        "compress_roofline": roofline("encode", z_bytes + n_bytes, t_c, bb, nb,
+                                      "lzo1x_encode_gdict_kernel"),
+        "step_ms": {"compress": round(t_c * 1e3, 4), "decompress": round(t_d * 1e3, 4)},
+        "decompress_gibps": round(dec_gibps, 3),
+        "compress_kernel_gibps": round(n_bytes / t_c / GIB, 3),      # this GPU, HIP events
         "errors": errors,
         "fallback_blocks": R.fallback_blocks,
     }
-    if world == 1 and args.workload == "c2":
-        # Successive batches pipelined on two streams: each launch's 4096
-        # blocks fill the chip in one round, so its first pieces (parser
-        # only) and last blocks leave SIMDs idle; overlapping the next
-        # batch's launch recovers them.  Reported beside `value`, which stays
-        # the one-launch-at-a-time rate.
+    if world == 1 and args.workload in ("c2", "c3"):
+        # Successive decode batches on two streams (each launch's 4096 blocks
+        # fill the chip in one round, so its first pieces and last blocks
+        # leave SIMDs idle; the next launch recovers them).  Reported beside
+        # the decode-only rate.
         p_wall, p_ok = R.pipelined(args.steps)
-        result["pipelined_gibps"] = round(n_all * args.steps / p_wall / GIB, 3)
-        result["pipelined_exact"] = p_ok
+        result["decompress_pipelined_gibps"] = round(n_all * args.steps / p_wall / GIB, 3)
+        result["decompress_pipelined_exact"] = p_ok
         errors += 0 if p_ok else 1
         result["errors"] = errors
-    if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c2":
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload in ("c2", "c3"):
         plain, comps = R.sample(min(len(mine), 512))
         result["cpu_baseline"] = cpu_baseline(plain, comps, args.cpu_seconds)
+        c1 = cpu_c1(synth, args.cpu_seconds / 2)
+        if c1:
+            result["cpu_baseline"]["c1"] = c1
     return result, errors
 
 
@@ -498,6 +628,61 @@ def run_c5(args, rank):
     return result, res["errors"]
 
 
+# ---------------------------------------------------------------------------
+# Single calls: the minilzo.h drop-in one block at a time
+# ---------------------------------------------------------------------------
+def run_single(args, lzo, synth):
+    """Per-call latency of lzo1x_1_compress / lzo1x_decompress (the unchanged
+    callers mds/itb.c:2923, :2964, mdsl/gc.c:770, api/api.c:6523/:6438) at the
+    smallest ITB, a 64 KiB block and the largest ITB payload, next to the
+    reference's lib/minilzo.c on one host core."""
+    lib = lzo.load()
+    ref = _ref_lib()
+    ulong = ctypes.c_ulong
+    out = {}
+    for n in (12416, 65536, 536192):
+        d = synth.block(synth.ITB, 777 + n, n)
+        src = ctypes.create_string_buffer(d, n)
+        z = ctypes.create_string_buffer(n + n // 16 + 128)
+        back = ctypes.create_string_buffer(n + 64)
+        wrk = ctypes.create_string_buffer(131072)
+        zl, ol = ulong(0), ulong(0)
+        row = {}
+        for name, L in (("gpu", lib), ("ref", ref)):
+            if L is None:
+                continue
+            reps = max(3, args.steps)
+            if name == "ref":
+                ctypes.memset(wrk, 0, 131072)
+            L.lzo1x_1_compress(src, n, z, ctypes.byref(zl), wrk)      # warm-up
+            L.lzo1x_decompress(z, zl.value, back, ctypes.byref(ol), None)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                if name == "ref":
+                    ctypes.memset(wrk, 0, 131072)               # zero-filled wrkmem, as defined
+                L.lzo1x_1_compress(src, n, z, ctypes.byref(zl), wrk)
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                rc = L.lzo1x_decompress(z, zl.value, back, ctypes.byref(ol), None)
+            t2 = time.perf_counter()
+            ok = rc == 0 and ol.value == n and back.raw[:n] == d
+            row[name] = {"compress_us": round((t1 - t0) / reps * 1e6, 1),
+                         "decompress_us": round((t2 - t1) / reps * 1e6, 1),
+                         "zlen": int(zl.value), "exact": ok}
+        out[str(n)] = row
+    v = out["65536"]["gpu"]["decompress_us"]
+    errors = sum(0 if r.get("exact", True) else 1 for row in out.values() for r in row.values())
+    result = {
+        "metric": "LZO1X single-call latency, lzo1x_decompress of one 64 KiB ITB block (us)",
+        "value": v, "unit": "us", "n_gpus": 1, "steps": max(3, args.steps), "warmup": 1,
+        "higher_is_better": False, "scaling": "none", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic ITB payload images", "config": {
+            "workload": "minilzo.h single calls (host buffers in, host buffers out: H2D, "
+                        "kernels, D2H, one stream sync per call) vs lib/minilzo.c on one core"},
+        "calls": out}
+    return result, errors
+
+
 def main():
     args = parse()
     import torch
@@ -525,6 +710,8 @@ def main():
     lzo.load()
     if args.workload == "c5":
         result, errors = run_c5(args, rank)
+    elif args.workload == "single":
+        result, errors = run_single(args, lzo, synth)
     else:
         result, errors = run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank,
                                       backend)
