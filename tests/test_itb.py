@@ -129,3 +129,50 @@ def test_itb_decompress_reports_bad_stream():
     err, ok = itb.decompress_batch([tmp])
     assert err[0] != 0 and ok == [0]
     assert itb.header_fields(tmp)[2] == itb.COMPR_NONE      # flag cleared regardless
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("win", [64 << 20, 1 << 20])
+def test_c5_append_file_loop_on_gpu(oracle, tmp_path, win):
+    """configs[4] (C5) end to end, as the MDS and MDSL do it: ITB records ->
+    pom_itb_lzo_compress_batch (mds/itb.c:2904-2945, GPU) -> the records as
+    sent (compressed ones from tmp, incompressible ones as they were) ->
+    pom_abuf_append_batch into the MDSL append file (mdsl/storage.c:455-519) ->
+    pom_itb_read, header then payload (mdsl/m2ml.c:124-273) ->
+    pom_itb_lzo_decompress_batch in place (mds/itb.c:2949-2980, GPU).  Each
+    stored record is byte-identical to the reference's itb_lzo_compress
+    (restated with the oracle's payload), and each record read back and
+    decoded is the original but for h.zlen, which itb_lzo_decompress leaves
+    holding the uncompressed length."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    recs = _records(40, seed=11) + _records(3, seed=12, model=synth.RANDOM)
+    originals = [bytes(r[: itb.header_fields(r)[0]]) for r in recs]
+    tmps = [bytearray(itb.ITB_FULL) for _ in recs]
+    which, err = itb.compress_batch(recs, tmps)
+    assert err == [0] * len(recs)
+    sent = [t if w else r for r, t, w in zip(recs, tmps, which)]
+    for o, w, orig in zip(sent, which, originals):
+        ew, erec = _expected_compress(oracle, bytearray(orig))
+        assert w == ew and bytes(o[: itb.header_fields(o)[0]]) == erec
+    path = str(tmp_path / "c5.itb")
+    af = itb.AppendFile(path, win=win)
+    locs = af.append_batch(sent, [itb.header_fields(o)[0] for o in sent])
+    af.close()
+    assert os.path.getsize(path) == sum(itb.header_fields(o)[0] for o in sent)
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        back = [itb.read_record(fd, loc) for loc in locs]
+    finally:
+        os.close(fd)
+    comp = [i for i, b in enumerate(back) if itb.header_fields(b)[2] == itb.COMPR_LZO]
+    assert len(comp) == sum(which) >= 40
+    derr, ok = itb.decompress_batch([back[i] for i in comp])
+    assert derr == [0] * len(comp) and ok == [1] * len(comp)
+    for b, orig in zip(back, originals):
+        ln, _, algo = itb.header_fields(b)
+        assert algo == itb.COMPR_NONE and ln == len(orig)
+        h = bytearray(b[: itb.ITBH_SIZE])
+        h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = orig[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
+        assert bytes(h) + bytes(b[itb.ITBH_SIZE: ln]) == orig
