@@ -82,6 +82,15 @@ int lzo_mi355x_compress_batch(const uint8_t *const *src, const size_t *src_len,
 int lzo_mi355x_decompress_batch(const uint8_t *const *src, const size_t *src_len,
                                 uint8_t *const *dst, size_t *dst_len, int *status,
                                 size_t nblocks);
+/* As lzo_mi355x_decompress_batch, for blocks made of consecutive LZO1X
+ * streams: the hvfs_fwritev column layout (api/api.c:6666-6680, one
+ * lzo1x_1_compress stream per iovec, back to back).  Each stream decodes as
+ * its own lzo1x_decompress_safe call would, right after the previous one's
+ * output; dst_len[b] is the total and status[b] the last stream's code (0
+ * when the last stream ends exactly at the end of the block). */
+int lzo_mi355x_decompress_concat_batch(const uint8_t *const *src, const size_t *src_len,
+                                       uint8_t *const *dst, size_t *dst_len, int *status,
+                                       size_t nblocks);
 
 #ifdef __cplusplus
 }

@@ -15,8 +15,11 @@
  *     output never exceeds the caller's capacity;
  *   - hvfs_fwritev compresses each iovec into its own stream and
  *     concatenates them, which the read side (one lzo1x_decompress call)
- *     cannot decode (INPUT_NOT_CONSUMED after the first stream): here the
- *     iovecs form one stream, which that same read side decodes.
+ *     cannot decode (INPUT_NOT_CONSUMED after the first stream).  Here
+ *     pom_col_zipv writes the iovecs as one stream, which that same read side
+ *     decodes, and pom_col_unzip_batch also reads the reference writer's
+ *     layout (consecutive streams until the input is used up), so columns the
+ *     reference already wrote stay readable.
  */
 #ifndef POM_COLUMN_H
 #define POM_COLUMN_H 1
@@ -46,9 +49,10 @@ int pom_col_zipv(const uint8_t *const *iov_base, const size_t *iov_len, size_t i
                  uint8_t *zip, size_t zip_cap, size_t *zip_len, int *compressed);
 
 /* n zipped columns -> out[b] (capacity out_cap[b]).  err[b] = 0 when the
- * stream decodes to exactly its recorded length, else the decoder's LZO_E_*
- * code, or LZO_E_ERROR for a length mismatch or a column shorter than its
- * header.  out_len[b] = bytes produced. */
+ * stream (or the reference fwritev layout's consecutive streams) decodes to
+ * exactly its recorded length, else the decoder's LZO_E_* code, or
+ * LZO_E_ERROR for a length mismatch or a column shorter than its header.
+ * out_len[b] = bytes produced. */
 int pom_col_unzip_batch(const uint8_t *const *zip, const size_t *zip_len, size_t n,
                         uint8_t *const *out, const size_t *out_cap, size_t *out_len, int *err);
 

@@ -91,6 +91,12 @@ int pom_col_zipv(const uint8_t *const *iov_base, const size_t *iov_len, size_t i
     return rc;
 }
 
+/* Columns are first decoded as one stream each (what pom_col_zip_batch and
+ * pom_col_zipv write, and what the reference reader expects,
+ * api/api.c:6438-6446).  A column whose first stream ends short of the input
+ * (INPUT_NOT_CONSUMED) is the reference writer's
+ * hvfs_fwritev layout (api/api.c:6666-6680, one stream per iovec): it is
+ * decoded again as consecutive streams until the input is used up. */
 int pom_col_unzip_batch(const uint8_t *const *zip, const size_t *zip_len, size_t n,
                         uint8_t *const *out, const size_t *out_cap, size_t *out_len, int *err)
 {
@@ -101,8 +107,15 @@ int pom_col_unzip_batch(const uint8_t *const *zip, const size_t *zip_len, size_t
     size_t *dlen = malloc(n * sizeof(*dlen));
     uint64_t *want = malloc(n * sizeof(*want));
     int *st = malloc(n * sizeof(*st));
+    size_t *multi = malloc(n * sizeof(*multi));
+    const uint8_t **msrc = malloc(n * sizeof(*msrc));
+    size_t *mslen = malloc(n * sizeof(*mslen));
+    uint8_t **mdst = malloc(n * sizeof(*mdst));
+    size_t *mdlen = malloc(n * sizeof(*mdlen));
+    int *mst = malloc(n * sizeof(*mst));
     int rc = LZO_E_OUT_OF_MEMORY;
-    if (!src || !slen || !dlen || !want || !st)
+    if (!src || !slen || !dlen || !want || !st || !multi || !msrc || !mslen || !mdst || !mdlen ||
+        !mst)
         goto out;
     for (size_t b = 0; b < n; b++) {
         want[b] = 0;
@@ -115,6 +128,25 @@ int pom_col_unzip_batch(const uint8_t *const *zip, const size_t *zip_len, size_t
     rc = lzo_mi355x_decompress_batch(src, slen, out, dlen, st, n);
     if (rc != LZO_E_OK)
         goto out;
+    size_t nm = 0;
+    for (size_t b = 0; b < n; b++)
+        if (zip_len[b] >= POM_COL_HDR && st[b] == LZO_E_INPUT_NOT_CONSUMED) {
+            multi[nm] = b;
+            msrc[nm] = src[b];
+            mslen[nm] = slen[b];
+            mdst[nm] = out[b];
+            mdlen[nm] = out_cap[b];
+            nm++;
+        }
+    if (nm) {
+        rc = lzo_mi355x_decompress_concat_batch(msrc, mslen, mdst, mdlen, mst, nm);
+        if (rc != LZO_E_OK)
+            goto out;
+        for (size_t k = 0; k < nm; k++) {
+            dlen[multi[k]] = mdlen[k];
+            st[multi[k]] = mst[k];
+        }
+    }
     for (size_t b = 0; b < n; b++) {
         out_len[b] = dlen[b] < out_cap[b] ? dlen[b] : out_cap[b];
         if (zip_len[b] < POM_COL_HDR)
@@ -130,5 +162,11 @@ out:
     free(dlen);
     free(want);
     free(st);
+    free(multi);
+    free(msrc);
+    free(mslen);
+    free(mdst);
+    free(mdlen);
+    free(mst);
     return rc;
 }

@@ -378,6 +378,47 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
     }
 }
 
+// Block b holds consecutive LZO1X streams, each decoded as by its own
+// lzo1x_decompress_safe call into the output right after the previous one's
+// (the hvfs_fwritev column layout, api/api.c:6666-6680: one lzo1x_1_compress
+// stream per iovec, back to back).  A stream that ends before the input does
+// (INPUT_NOT_CONSUMED, the :3676-3680 boundary) is followed by the next;
+// any other code ends the block with it.  out_len = bytes of all streams.
+__global__ __launch_bounds__(kWave) void lzo1x_decode_concat_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks)
+{
+    __shared__ uint8_t ring[kRing];
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t len = src_len[b], cap = dst_cap[b];
+    uint32_t pos = 0, produced = 0;
+    int rc;
+    do {
+        Dec<true> d;
+        d.W.in = src + src_off[b] + pos;
+        d.W.len = len - pos;
+        d.W.r0 = -((int64_t)1 << 40);
+        d.W.w = 0;
+        d.ring = ring;
+        d.out = dst + dst_off[b] + produced;
+        d.cap = cap - produced;
+        d.ip = d.op = d.flushed = 0;
+        d.unchecked = false;
+        rc = dec_run(d);
+        dec_flush(d, d.op);
+        produced += d.op;
+        pos += d.ip;                               // >= 3 per stream (the EOF marker)
+    } while (rc == E_INPUT_NOT_CONSUMED);
+    if (lane_id() == 0) {
+        out_len[b] = produced;
+        status[b] = rc;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Encoder: LZO1X-1 greedy parse with the dictionary
 // in LDS.  The wave probes 64 consecutive positions at once; lanes whose
@@ -611,6 +652,20 @@ extern "C" int lzo_mi355x_launch_decompress_exact(const uint8_t* src, const uint
     hipLaunchKernelGGL(lzo1x_decode_exact_kernel<true>, dim3(ngrid), dim3(kWave), 0, stream, src,
                        src_off, src_len, dst, dst_off, dst_cap, out_len, status, fb, nblocks,
                        unchecked != 0, 0xFFFFFFFFu, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzo_mi355x_launch_decompress_concat(const uint8_t* src, const uint64_t* src_off,
+                                                   const uint32_t* src_len, uint8_t* dst,
+                                                   const uint64_t* dst_off,
+                                                   const uint32_t* dst_cap, uint32_t* out_len,
+                                                   int32_t* status, uint32_t nblocks,
+                                                   hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_decode_concat_kernel, dim3(nblocks), dim3(kWave), 0, stream, src,
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -375,7 +375,7 @@ static void layout_fill(const struct layout *L, uint8_t *h, const uint8_t *const
     }
 }
 
-enum op_kind { OP_COMPRESS, OP_DECOMPRESS };
+enum op_kind { OP_COMPRESS, OP_DECOMPRESS, OP_CONCAT };
 
 /* Runs one staged batch.  dst_cap: capacities used by the kernels.  On
  * return out_len/status of each block are in the pinned staging. */
@@ -397,8 +397,10 @@ static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
     int rc;
     if (kind == OP_COMPRESS)
         rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, s);
-    else
+    else if (kind == OP_DECOMPRESS)
         rc = decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, 0, s);
+    else
+        rc = lzo_mi355x_launch_decompress_concat(dsrc, so, sl, ddst, dof, dc, ol, st, nb, s);
     if (rc != 0)
         return -1;
     if (hipMemcpyAsync(h + L->o_outlen, d + L->o_outlen, 8 * L->nb, hipMemcpyDeviceToHost, s) !=
@@ -522,6 +524,13 @@ int lzo_mi355x_decompress_batch(const uint8_t *const *src, const size_t *src_len
                                 size_t nblocks)
 {
     return batch_common(OP_DECOMPRESS, src, src_len, dst, dst_len, status, nblocks);
+}
+
+int lzo_mi355x_decompress_concat_batch(const uint8_t *const *src, const size_t *src_len,
+                                       uint8_t *const *dst, size_t *dst_len, int *status,
+                                       size_t nblocks)
+{
+    return batch_common(OP_CONCAT, src, src_len, dst, dst_len, status, nblocks);
 }
 
 /* ------------------------------------------------------------------------ */

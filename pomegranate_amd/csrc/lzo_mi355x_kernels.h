@@ -43,6 +43,15 @@ int lzo_mi355x_launch_decompress_exact(const uint8_t *src, const uint64_t *src_o
                                        const uint32_t *fb, uint32_t ngrid,
                                        uint32_t nblocks, int unchecked, hipStream_t stream);
 
+/* Exact decoder over blocks of consecutive streams (the hvfs_fwritev column
+ * layout): each stream decodes with lzo1x_decompress_safe semantics right
+ * after the previous one's output; out_len = the total. */
+int lzo_mi355x_launch_decompress_concat(const uint8_t *src, const uint64_t *src_off,
+                                        const uint32_t *src_len, uint8_t *dst,
+                                        const uint64_t *dst_off, const uint32_t *dst_cap,
+                                        uint32_t *out_len, int32_t *status, uint32_t nblocks,
+                                        hipStream_t stream);
+
 /* Throughput decoder (lzo1x_decode_fast.hip).  Blocks it does not finish
  * exactly are appended to fb (fb[0] = count, must be 0 on entry) and get
  * status 0x7FFF0001 until the exact decoder runs on them.  ops: device

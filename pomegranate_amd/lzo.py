@@ -46,6 +46,7 @@ EXPORTS = (
     "lzo_mi355x_decompress_scratch", "lzo_mi355x_decoded_length_dev",
     "lzo_mi355x_compress_scratch",
     "lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
+    "lzo_mi355x_decompress_concat_batch",
     # include/pom_itb.h
     "pom_itb_lzo_compress_batch", "pom_itb_lzo_decompress_batch",
     "pom_abuf_open", "pom_abuf_append", "pom_abuf_append_batch", "pom_abuf_close", "pom_itb_read",
@@ -107,7 +108,8 @@ def load() -> ctypes.CDLL:
     lib.lzo_mi355x_decompress_scratch.argtypes = [ctypes.c_uint32]
     lib.lzo_mi355x_decoded_length_dev.restype = ctypes.c_int
     lib.lzo_mi355x_decoded_length_dev.argtypes = [_u8p] * 5 + [ctypes.c_uint32, _u8p]
-    for name in ("lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch"):
+    for name in ("lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
+                 "lzo_mi355x_decompress_concat_batch"):
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
         fn.argtypes = [_u8p, _u8p, _u8p, _u8p, _u8p, _size]
@@ -191,8 +193,9 @@ def compress_batch(blocks: Sequence[bytes]) -> Tuple[int, List[int], List[bytes]
     return rc, list(st), [dsts[i].raw[: dlen[i]] for i in range(nb)]
 
 
-def decompress_batch(blocks: Sequence[bytes], caps: Sequence[int]
+def decompress_batch(blocks: Sequence[bytes], caps: Sequence[int], concat: bool = False
                      ) -> Tuple[int, List[int], List[bytes]]:
+    """concat: blocks of consecutive streams (lzo_mi355x_decompress_concat_batch)."""
     lib = load()
     nb = len(blocks)
     srcs = [ctypes.create_string_buffer(bytes(b), max(len(b), 1)) for b in blocks]
@@ -200,7 +203,8 @@ def decompress_batch(blocks: Sequence[bytes], caps: Sequence[int]
     slen = (_size * nb)(*[len(b) for b in blocks])
     dlen = (_size * nb)(*caps)
     st = (ctypes.c_int * nb)()
-    rc = lib.lzo_mi355x_decompress_batch(_ptr_array(srcs), slen, _ptr_array(dsts), dlen, st, nb)
+    fn = lib.lzo_mi355x_decompress_concat_batch if concat else lib.lzo_mi355x_decompress_batch
+    rc = fn(_ptr_array(srcs), slen, _ptr_array(dsts), dlen, st, nb)
     return rc, list(st), [dsts[i].raw[: min(dlen[i], caps[i])] for i in range(nb)]
 
 

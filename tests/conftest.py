@@ -111,6 +111,24 @@ def unchecked():
 
 
 @pytest.fixture(scope="session")
+def fwritev_columns():
+    """Columns as the reference's hvfs_fwritev writes them (api/api.c:6652-6689):
+    [u64 length] + one reference lzo1x_1_compress stream per iovec, with what
+    the reference's read side returns on them (tests/golden/make_golden.py)."""
+    z = np.load(os.path.join(GOLDEN, "column.npz"))
+    n_iov = [int(n) for n in z["n_iov"]]
+    flat = [int(n) for n in z["iov_len"]]
+    sizes, at = [], 0
+    for n in n_iov:
+        sizes.append(flat[at: at + n])
+        at += n
+    return {"names": [str(s) for s in z["names"]], "iov_len": sizes,
+            "data": _unpack(z["data"], z["data_off"]), "zips": _unpack(z["z_data"], z["z_off"]),
+            "read_rc": [int(r) for r in z["read_rc"]],
+            "read_len": [int(n) for n in z["read_len"]]}
+
+
+@pytest.fixture(scope="session")
 def manifest():
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         return json.load(f)["batches"]

@@ -20,6 +20,11 @@ repository).  Every vector below is the reference's own output:
                  marker is cut short: return code (:3676-3680), *out_len and
                  the SHA-256 of the produced bytes; inputs zero padded past
                  their end
+  column.npz     columns as the reference's hvfs_fwritev writes them with
+                 SCD_LZO (api/api.c:6652-6689): [u64 length] then one
+                 lzo1x_1_compress stream per iovec, back to back; with the
+                 iovec sizes, the data, and what the reference's read side
+                 (one lzo1x_decompress call, :6438-6446) returns on it
 
 Run:  make -C oracle && python tests/golden/make_golden.py
 """
@@ -215,6 +220,44 @@ def unchecked_cases(ref: Ref):
     return {int(k): rcs.count(k) for k in set(rcs)}
 
 
+def column_cases(ref: Ref):
+    """hvfs_fwritev columns (api/api.c:6652-6689) from the reference codec."""
+    rng = random.Random(6666)
+    shapes = [
+        ("one_iov", [4096]),
+        ("two_iov", [4096, 12288]),
+        ("fuse_pages", [4096] * 5),
+        ("empty_iov", [3000, 0, 5000]),
+        ("fuse_buffer", [4096] * 40),
+        ("tiny_iovs", [37] * 100),
+        ("big_then_small", [200000, 100, 7, 3000]),
+        ("ragged", [rng.randrange(1, 9000) for _ in range(12)]),
+        ("trailing_empty", [8192, 0]),
+    ]
+    names, iov_len, iov_data, zips, rd_rc, rd_len = [], [], [], [], [], []
+    for i, (name, sizes) in enumerate(shapes):
+        iov = [synth.block((synth.ITB, synth.TEXT, synth.LZLIKE)[(i + k) % 3], 20000 + 50 * i + k, n)
+               for k, n in enumerate(sizes)]
+        total = sum(sizes)
+        payload = b"".join(ref.compress(v) for v in iov)
+        assert len(payload) + 8 < total          # compressed: not sent raw (:6681-6685)
+        zips.append(total.to_bytes(8, "little") + payload)
+        rc, out = ref.decompress_unchecked(payload, total + 4096)
+        names.append(name)
+        iov_len.append(np.array(sizes, np.int64))
+        iov_data.append(b"".join(iov))
+        rd_rc.append(rc)
+        rd_len.append(len(out))
+    nl = np.array([len(v) for v in iov_len], np.int64)
+    dd, do = pack(iov_data)
+    zd, zo = pack(zips)
+    np.savez_compressed(os.path.join(OUT, "column.npz"), names=np.array(names), n_iov=nl,
+                        iov_len=np.concatenate(iov_len), data=dd, data_off=do, z_data=zd,
+                        z_off=zo, read_rc=np.array(rd_rc, np.int32),
+                        read_len=np.array(rd_len, np.int64))
+    return {n: (r, l) for n, r, l in zip(names, rd_rc, rd_len)}
+
+
 def batch_entry(ref: Ref, name, model, seed0, sizes, note):
     arena, offs, lens = synth.batch(model, seed0, sizes)
     hz, hi = hashlib.sha256(), hashlib.sha256()
@@ -259,6 +302,7 @@ def main():
     print("edge vectors:", edge_cases(ref))
     print("malformed rc histogram:", malformed_cases(ref))
     print("unchecked rc histogram:", unchecked_cases(ref))
+    print("column reader (rc, olen):", column_cases(ref))
     print("manifest:", manifest(ref))
 
 

@@ -9,7 +9,7 @@ import struct
 import numpy as np
 import pytest
 
-from pomegranate_amd import column, synth
+from pomegranate_amd import column, lzo, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -72,3 +72,45 @@ def test_zipv_is_one_decodable_stream(oracle):
     assert k == 1 and z == struct.pack("<Q", len(flat)) + oracle.compress(flat)
     outs, err = column.unzip_batch([z], [len(flat)])
     assert err == [0] and outs == [flat]
+
+
+def test_unzip_reads_reference_fwritev_columns(fwritev_columns):
+    """Columns the reference's hvfs_fwritev wrote (api/api.c:6666-6680, one
+    stream per iovec; reference-generated fixtures) decode to their data,
+    where the reference's own read side stops after the first stream."""
+    fx = fwritev_columns
+    outs, err = column.unzip_batch(fx["zips"], [len(d) for d in fx["data"]])
+    assert err == [0] * len(outs)
+    assert outs == fx["data"]
+    # mixed with single-stream columns and in a tight capacity
+    zips, comp = column.zip_batch([fx["data"][2], fx["data"][4]])
+    assert comp == [1, 1]
+    outs, err = column.unzip_batch([zips[0], fx["zips"][4], zips[1], fx["zips"][6]],
+                                   [len(fx["data"][i]) for i in (2, 4, 4, 6)])
+    assert err == [0] * 4 and outs == [fx["data"][i] for i in (2, 4, 4, 6)]
+
+
+def test_unzip_fwritev_columns_errors(fwritev_columns):
+    """Damaged multi-stream columns fail like a damaged single stream: the
+    last stream cut short, too little room, or a recorded length that the
+    streams do not add up to."""
+    fx = fwritev_columns
+    i = fx["names"].index("fuse_pages")
+    z, d = fx["zips"][i], fx["data"][i]
+    bad_len = struct.pack("<Q", len(d) + 1) + z[8:]
+    outs, err = column.unzip_batch([z[:-2], z, bad_len], [len(d), len(d) - 1, len(d) + 1])
+    assert err[0] != 0 and err[1] == -5 and err[2] != 0
+    assert outs[1] == d[:len(d) - 1][: len(outs[1])]
+
+
+def test_concat_batch_matches_per_stream_decodes(fwritev_columns):
+    """lzo_mi355x_decompress_concat_batch: each stream decodes as its own
+    lzo1x_decompress_safe call would; the status is the last stream's."""
+    fx = fwritev_columns
+    payloads = [z[8:] for z in fx["zips"]]
+    rc, st, outs = lzo.decompress_batch(payloads, [len(d) for d in fx["data"]], concat=True)
+    assert rc == 0 and st == [0] * len(payloads) and outs == fx["data"]
+    # trailing junk after the last stream: INPUT_NOT_CONSUMED is not a stream start
+    rc, st, outs = lzo.decompress_batch([payloads[1] + b"\x00"], [len(fx["data"][1]) + 64],
+                                        concat=True)
+    assert rc == 0 and st[0] != 0

@@ -55,6 +55,25 @@ def test_oracle_matches_unchecked_decoder(oracle, unchecked):
     assert {("valid", 0), ("trailing", -8), ("concat2", -8), ("eof_cut", -4)} <= kinds
 
 
+def test_oracle_pins_fwritev_columns(oracle, fwritev_columns):
+    """The reference's hvfs_fwritev columns (api/api.c:6666-6680): the payload
+    is the oracle's per-iovec streams back to back, and the reference's read
+    side (one unchecked lzo1x_decompress, :6438-6446) stops after the first
+    stream with INPUT_NOT_CONSUMED whenever there is more than one."""
+    fx = fwritev_columns
+    for name, sizes, data, z, rc, n in zip(fx["names"], fx["iov_len"], fx["data"], fx["zips"],
+                                           fx["read_rc"], fx["read_len"]):
+        assert int.from_bytes(z[:8], "little") == len(data) == sum(sizes), name
+        iov, at = [], 0
+        for s in sizes:
+            iov.append(data[at: at + s])
+            at += s
+        assert z[8:] == b"".join(oracle.compress(v) for v in iov), name
+        assert (rc, n) == ((0, len(data)) if len(sizes) == 1 else (-8, sizes[0])), name
+        got_rc, got = oracle.decompress_unchecked(z[8:])
+        assert (got_rc, got) == (rc, data[:n]), name
+
+
 @pytest.mark.parametrize("name", ["C2C3", "C4_sample", "itb_max", "random_300k",
                                   "models64k_random", "models64k_itb", "models64k_zeros",
                                   "models64k_alpha4", "models64k_lzlike", "models64k_text"])
