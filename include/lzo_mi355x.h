@@ -47,7 +47,11 @@ size_t lzo_mi355x_compress_scratch(uint32_t nblocks);
 
 /* Decompression with lzo1x_decompress_safe semantics per block (capacity
  * dst_cap[b]).  `scratch` is device memory of lzo_mi355x_decompress_scratch()
- * bytes for nblocks (may be NULL when that is 0). */
+ * bytes for nblocks, or NULL (every block then takes the exact one-wave
+ * decoder).  The scratch holds a 4-byte-a-block list plus op slots for the
+ * workgroups resident at once (not per block): about 100 MB plus 4 bytes a
+ * block.  After the call, the u32 at scratch byte 0 counts the blocks the
+ * throughput decoder handed to the exact decoder (diagnostic). */
 int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
                               const uint32_t *src_len, uint8_t *dst,
                               const uint64_t *dst_off, const uint32_t *dst_cap,
@@ -68,17 +72,23 @@ int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len,
 
 /* ---- host-resident batches --------------------------------------------------
  * Blocks start and end in host memory (the mdsl/aio.c write path and the
- * xnet wire).  Blocks are packed into pinned staging, copied to the GPU with
- * hipMemcpyAsync, coded, and copied back.  Synchronous; thread-safe (each
- * host thread owns its stream and staging).  Returns 0, or LZO_E_ERROR when
- * the GPU is unusable; per-block results are in status[].
+ * xnet wire).  The blocks are ordered largest first and dealt round robin
+ * over the GPUs (POM_LZO_DEVICES, default all; a batch below 64 MiB a GPU
+ * stays on the caller's current GPU).  Each GPU's share is cut into chunks of
+ * at most 128 MiB of input plus output capacity (POM_LZO_CHUNK_MB; the first
+ * chunk a quarter of that), each packed into pinned staging, copied to the
+ * GPU with hipMemcpyAsync, coded and copied back, up to four chunks in flight
+ * on four streams, so staging stays bounded whatever the batch size.
+ * Synchronous; thread-safe (each host thread owns its streams and staging on
+ * each GPU).  Returns 0, or LZO_E_ERROR when a GPU is unusable (its blocks
+ * then read LZO_E_ERROR); per-block results are in status[].
  */
 int lzo_mi355x_compress_batch(const uint8_t *const *src, const size_t *src_len,
                               uint8_t *const *dst, size_t *dst_len, int *status,
                               size_t nblocks);
-/* dst_len[b] is the capacity in and the produced length out.  Both batch
- * calls stage every input before they write any output, so dst[b] may overlap
- * src[b] (in-place decoding). */
+/* dst_len[b] is the capacity in and the produced length out.  A block's
+ * input is staged before its output is written, so dst[b] may overlap src[b]
+ * (in-place decoding); it must not overlap another block's input. */
 int lzo_mi355x_decompress_batch(const uint8_t *const *src, const size_t *src_len,
                                 uint8_t *const *dst, size_t *dst_len, int *status,
                                 size_t nblocks);

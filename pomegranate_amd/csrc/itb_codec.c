@@ -113,8 +113,8 @@ int pom_itb_lzo_decompress_batch(uint8_t *const *in, const size_t *cap, int *err
         const uint32_t len = rd32(in[b] + POM_ITBH_LEN_OFF);
         slen[b] = len >= POM_ITBH_SIZE ? len - POM_ITBH_SIZE : 0;
     }
-    /* in place: the batch call stages every payload before it writes any
-     * output (include/lzo_mi355x.h), so no copy aside is needed */
+    /* in place: the batch call stages a block's payload before it writes that
+     * block's output (include/lzo_mi355x.h), so no copy aside is needed */
     for (size_t b = 0; b < n; b++) {
         src[b] = in[b] + POM_ITBH_SIZE;
         dst[b] = in[b] + POM_ITBH_SIZE;

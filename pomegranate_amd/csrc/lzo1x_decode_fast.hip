@@ -126,7 +126,7 @@ constexpr uint32_t kInfoErr = 1u << 17;          // piece info: the block needs 
 constexpr uint32_t kStepSpan = 16 * kWave + 16;
 // (diagnostics: why, in bits 20..23 of the piece info / the CN_REASON stamp)
 enum { RS_NONE, RS_OFF_END, RS_BAD, RS_OPS, RS_DEAD, RS_EWAIT, RS_OVERRUN, RS_LOOKBEHIND,
-       RS_SPACE, RS_LANDED, RS_HEAD };
+       RS_SPACE, RS_LANDED, RS_HEAD, RS_WRITER };
 
 // parse states (instruction starts)
 constexpr uint32_t ST_A = 0;   // top: t < 16 is a literal run
@@ -164,6 +164,9 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t parsed;          // parser -> executor: pieces whose ops are in their slot
     uint32_t consumed;        // executor -> parser: pieces whose slot is free again
     uint32_t pinfo[kSlots];   // per slot: op count | kInfoEof | kInfoErr
+    uint32_t opset;           // this workgroup's op-slot set (from the pool)
+    uint32_t done;            // waves done with the block (the second one closes it)
+    uint32_t why;             // executor's refusal reason
 };
 
 constexpr uint32_t kRingOff = 0;                                  // offsetof(FastLds, ring)
@@ -1232,14 +1235,103 @@ __device__ __forceinline__ void src_commit(FastLds& S, uint32_t l, const SrcCopy
 }
 
 // ---------------------------------------------------------------------------
+// Op-slot pool.  The scratch holds `nsets` op-slot sets, as many as there are
+// workgroups resident at once, not one per block.  A workgroup takes a set
+// when it starts and returns it when both its waves are done.  The sets are
+// split over kPoolParts partitions (block b uses partition b mod parts) so
+// that the workgroups starting together do not all hit one atomic counter;
+// within partition p (count_p sets p, p + parts, ...):
+//   take:   i = take_p++; i < count_p is set p + i * parts, fresh; a later i
+//           waits for partition p's (i - count_p)-th return, published in ring
+//           entry (i - count_p) mod count_p as {sequence number + 1, set};
+//   return: j = ret_p++; that ring entry for j = {j + 1, set}.
+// A workgroup waits only while every set of its partition is held by a
+// running workgroup (resident, so it finishes): no deadlock, whatever the
+// occupancy or dispatch order.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPoolParts = 32;
+constexpr uint32_t kPoolStride = 64;             // u32 words per partition (256 B: two 128-B lines)
+
+static_assert(kPoolParts * kPoolStride * 4 == LZO_MI355X_FAST_POOL_BYTES, "pool counters");
+
+struct OpPool {
+    uint32_t* ctr;                               // [parts][kPoolStride]: take at 0, return at 32
+    unsigned long long* ring;                    // entry p + k * parts: partition p's k-th slot
+    uint32_t nsets;
+};
+
+__device__ __forceinline__ uint32_t pool_parts(uint32_t nsets)
+{
+    return nsets < kPoolParts ? nsets : kPoolParts;
+}
+
+__device__ uint32_t opset_take(const OpPool& P, uint32_t b)
+{
+    const uint32_t parts = pool_parts(P.nsets), p = b % parts;
+    const uint32_t count = (P.nsets - p + parts - 1) / parts;
+    const uint32_t i = atomicAdd(&P.ctr[p * kPoolStride], 1u);
+    if (i < count)
+        return p + i * parts;
+    const uint32_t j = i - count;
+    const unsigned long long want = (unsigned long long)(j + 1) << 32;
+    unsigned long long* const e = &P.ring[p + (j % count) * parts];
+    for (;;) {
+        // relaxed: only the set number passes (an acquire would invalidate the L2)
+        const unsigned long long v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & ~0xFFFFFFFFull) == want)
+            return (uint32_t)v;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+__device__ void opset_return(const OpPool& P, uint32_t set)
+{
+    const uint32_t parts = pool_parts(P.nsets), p = set % parts;
+    const uint32_t count = (P.nsets - p + parts - 1) / parts;
+    const uint32_t j = atomicAdd(&P.ctr[p * kPoolStride + 32], 1u);
+    // relaxed: the op slots carry nothing to the next user, and every access
+    // to them has completed (the parser waits for its stores before publishing
+    // a piece; the executor has used what it read).  A release here would write
+    // back the XCD's whole L2 (the block's fresh output) once per block.
+    __hip_atomic_store(&P.ring[p + (j % count) * parts], ((unsigned long long)(j + 1) << 32) | set,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lane 0 of each wave when it is done with block b.  The second wave out
+// publishes the block -- by then the executor has decided (state 1: finished,
+// 2: refused) and the writer has landed what it could -- and returns the op
+// set.  A writer that gave up (it polls for a bounded time) leaves bytes
+// unstored: that block goes to the exact decoder like any refusal.
+__device__ void block_close(FastLds& S, uint32_t b, uint32_t* __restrict__ out_len,
+                            int32_t* __restrict__ status, uint32_t* __restrict__ fallback,
+                            uint32_t* __restrict__ fallback_ids, const OpPool& P)
+{
+    if (__hip_atomic_fetch_add(&S.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        return;                                    // the other wave closes the block
+    const uint32_t st = lds_load(&S.state);
+    const uint32_t prod = lds_load(&S.produced);
+    if (st == 1 && lds_load(&S.landed) == prod) {
+        out_len[b] = prod;
+        status[b] = 0;
+    } else {
+        status[b] = kFallback;
+        out_len[b] = 0xFA110000u | (st == 2 ? lds_load(&S.why) : (uint32_t)RS_WRITER);  // (diagnostics)
+        const uint32_t at = atomicAdd(&fallback[0], 1u);
+        fallback_ids[at] = b;
+    }
+    opset_return(P, S.opset);
+}
+
 template <bool STAMPS>
 __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-    uint32_t* __restrict__ fallback, uint2* __restrict__ ops, uint32_t nblocks,
-    uint32_t prio_from, uint64_t* __restrict__ stamps)
+    uint32_t* __restrict__ fallback, uint32_t* __restrict__ fallback_ids,
+    uint2* __restrict__ ops, uint32_t nblocks,
+    uint32_t prio_from, uint64_t* __restrict__ stamps, uint32_t* __restrict__ pool,
+    unsigned long long* __restrict__ ring, uint32_t nsets)
 {
     __shared__ FastLds S;
     const uint32_t b = blockIdx.x;
@@ -1256,6 +1348,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         S.state = 0;
         S.parsed = 0;
         S.consumed = 0;
+        S.done = 0;
+        S.opset = opset_take(OpPool{pool, ring, nsets}, b);
     }
     if (threadIdx.x < kWave)
         S.flags[threadIdx.x] = 0;             // chunk tags start at 0x80000001
@@ -1279,7 +1373,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     k.cap = dst_cap[b];
     k.P = 0;
     k.staged = 0;
-    uint2* const gops = ops + (size_t)b * (kSlots * kOpMax);
+    uint2* const gops = ops + (size_t)__builtin_amdgcn_readfirstlane(S.opset) * (kSlots * kOpMax);
 
     // The exact decoder takes: destinations not 16-byte aligned, empty or huge
     // blocks (lengths up to 255 * z must not wrap 32 bits).
@@ -1294,6 +1388,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             for (int i = 0; i < PH_N; i++)
                 if (parser_slot(i))
                     stamps[(size_t)b * kStampSlots + i] = acc[i];
+        if (l == 0)
+            block_close(S, b, out_len, status, fallback, fallback_ids, OpPool{pool, ring, nsets});
         return;
     }
 
@@ -1650,59 +1746,66 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 stamps[(size_t)b * kStampSlots + i] = acc[i];
     if (l == 0) {
         if (refuse) {
+            lds_store(&S.why, reason);
             lds_store(&S.state, 2u);
-            status[b] = kFallback;
-            out_len[b] = 0xFA110000u | reason;         // (diagnostics; the exact decoder rewrites it)
-            const uint32_t at = atomicAdd(&fallback[0], 1u);
-            fallback[1 + at] = b;
         } else {
             lds_store(&S.produced, carry);
             lds_store(&S.state, 1u);
-            out_len[b] = carry;
-            status[b] = 0;
         }
+        block_close(S, b, out_len, status, fallback, fallback_ids, OpPool{pool, ring, nsets});
     }
 }
 #undef STAMP
 
 }  // namespace
 
-// Op slots per block in the decompression scratch (lzo_host.c sizes it).
+// Op-slot sets: as many as workgroups are resident at once, 16 per CU (LDS
+// and 8 waves per SIMD).
+extern "C" uint32_t lzo_mi355x_fast_resident_blocks(void)
+{
+    static int cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return 256u * (2 * POM_WAVES_PER_EU);
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            return 256u * (2 * POM_WAVES_PER_EU);
+        cus[dev] = n;
+    }
+    return (uint32_t)cus[dev] * (2 * POM_WAVES_PER_EU);
+}
+
+// Bytes of one op-slot set (lzo_host.c sizes the scratch).
 extern "C" size_t lzo_mi355x_fast_ops_bytes_per_block(void)
 {
     return (size_t)kSlots * kOpMax * sizeof(uint2);
 }
 
-// First block of the launch's final round: blocks resident at once are 16
-// per CU (LDS and 8 waves per SIMD).
-static uint32_t prio_from(uint32_t nblocks)
+// First block of the final round: the last `resident` blocks.
+static uint32_t prio_from(uint32_t nblocks, uint32_t resident)
 {
-    static int cus[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-        return 0;
-    if (!cus[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            return 0;
-        cus[dev] = n;
-    }
-    const uint64_t resident = (uint64_t)cus[dev] * (2 * POM_WAVES_PER_EU);
-    return nblocks > resident ? (uint32_t)(nblocks - resident) : 0u;
+    return nblocks > resident ? nblocks - resident : 0u;
 }
 
 extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint64_t* src_off,
                                                  const uint32_t* src_len, uint8_t* dst,
                                                  const uint64_t* dst_off, const uint32_t* dst_cap,
                                                  uint32_t* out_len, int32_t* status,
-                                                 uint32_t* fallback, void* ops, uint32_t nblocks,
+                                                 uint32_t* fallback, uint32_t* fallback_ids,
+                                                 uint32_t* pool, void* ring, void* ops,
+                                                 uint32_t nsets, uint32_t nblocks,
                                                  hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
+    if (nsets == 0)
+        return -1;
     hipLaunchKernelGGL(lzo1x_decode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0,
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
-                       fallback, (uint2*)ops, nblocks, prio_from(nblocks), nullptr);
+                       fallback, fallback_ids, (uint2*)ops, nblocks,
+                       prio_from(nblocks, lzo_mi355x_fast_resident_blocks()), nullptr, pool,
+                       (unsigned long long*)ring, nsets);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1710,12 +1813,17 @@ extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint6
 extern "C" int lzo_mi355x_debug_decompress_fast_stamps(
     const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len, uint8_t* dst,
     const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* out_len, int32_t* status,
-    uint32_t* fallback, void* ops, uint32_t nblocks, uint64_t* stamps, hipStream_t stream)
+    uint32_t* fallback, uint32_t* fallback_ids, uint32_t* pool, void* ring, void* ops,
+    uint32_t nsets, uint32_t nblocks, uint64_t* stamps, hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
+    if (nsets == 0)
+        return -1;
     hipLaunchKernelGGL(lzo1x_decode_fast_kernel<true>, dim3(nblocks), dim3(2 * kWave), 0,
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
-                       fallback, (uint2*)ops, nblocks, prio_from(nblocks), stamps);
+                       fallback, fallback_ids, (uint2*)ops, nblocks,
+                       prio_from(nblocks, lzo_mi355x_fast_resident_blocks()), stamps, pool,
+                       (unsigned long long*)ring, nsets);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

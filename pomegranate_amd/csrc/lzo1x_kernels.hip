@@ -351,16 +351,16 @@ __device__ void decode_exact_block(const uint8_t* __restrict__ src, const uint64
     }
 }
 
-// fb == nullptr: grid entry b decodes block b.  Otherwise fb[0] blocks listed
-// at fb[1..] (the fast decoder's refusals) are decoded grid-stride.
+// fb == nullptr: grid entry b decodes block b.  Otherwise the *fb blocks
+// listed at fb_ids[] (the fast decoder's refusals) are decoded grid-stride.
 template <bool WRITE>
 __global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-    const uint32_t* __restrict__ fb, uint32_t nblocks, bool unchecked, uint32_t cap_limit,
-    uint32_t* __restrict__ cap_out)
+    const uint32_t* __restrict__ fb, const uint32_t* __restrict__ fb_ids, uint32_t nblocks,
+    bool unchecked, uint32_t cap_limit, uint32_t* __restrict__ cap_out)
 {
     __shared__ uint8_t ring[WRITE ? kRing : 4];
     if (!fb) {
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_exact_kernel(
     }
     const uint32_t count = fb[0];
     for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
-        const uint32_t b = fb[1 + i];
+        const uint32_t b = fb_ids[i];
         if (b < nblocks)
             decode_exact_block<WRITE>(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
                                       status, ring, b, unchecked, cap_limit, cap_out);
@@ -643,15 +643,15 @@ extern "C" int lzo_mi355x_launch_decompress_exact(const uint8_t* src, const uint
                                                   const uint32_t* src_len, uint8_t* dst,
                                                   const uint64_t* dst_off, const uint32_t* dst_cap,
                                                   uint32_t* out_len, int32_t* status,
-                                                  const uint32_t* fb, uint32_t ngrid,
-                                                  uint32_t nblocks, int unchecked,
+                                                  const uint32_t* fb, const uint32_t* fb_ids,
+                                                  uint32_t ngrid, uint32_t nblocks, int unchecked,
                                                   hipStream_t stream)
 {
     if (ngrid == 0)
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_exact_kernel<true>, dim3(ngrid), dim3(kWave), 0, stream, src,
-                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fb, nblocks,
-                       unchecked != 0, 0xFFFFFFFFu, nullptr);
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fb, fb_ids,
+                       nblocks, unchecked != 0, 0xFFFFFFFFu, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -679,7 +679,7 @@ extern "C" int lzo_mi355x_launch_decoded_length(const uint8_t* src, const uint64
         return 0;
     hipLaunchKernelGGL(lzo1x_decode_exact_kernel<false>, dim3(nblocks), dim3(kWave), 0, stream,
                        src, src_off, src_len, nullptr, nullptr, nullptr, out_len, status,
-                       nullptr, nblocks, true, cap_limit, cap_out);
+                       nullptr, nullptr, nblocks, true, cap_limit, cap_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

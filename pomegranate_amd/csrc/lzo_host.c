@@ -8,17 +8,21 @@
  * usable GPU returns LZO_E_ERROR and says why on stderr once.
  *
  * Threading: callers are MDS commit/service threads, the MDSL
- * GC thread and client threads.  Each host thread gets its own HIP stream and
- * its own device/pinned staging (grown on demand, freed at thread exit), so
- * concurrent calls never share device state.
+ * GC thread and client threads.  Each host thread gets, on each GPU it uses,
+ * two HIP streams with their own device/pinned staging (grown on demand up to
+ * one chunk, freed at thread exit), so concurrent calls never share device
+ * state.  A host batch spreads over the GPUs on one helper thread per GPU
+ * (batch_split.c), which use the calling thread's per-GPU resources.
  */
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
+#include "batch_split.h"
 #include "lzo_mi355x.h"
 #include "lzo_mi355x_kernels.h"
 #include "minilzo.h"
@@ -54,16 +58,32 @@ size_t lzo_mi355x_worst_compress(size_t n)
 }
 
 /* ------------------------------------------------------------------------ */
-/* Per-thread stream and staging                                            */
+/* Per-thread, per-device streams and staging                               */
 /* ------------------------------------------------------------------------ */
-struct tctx {
-    int ready;
-    int device;
+/* A staging slot: one stream with its device and pinned host buffers (grown
+ * on demand; a host batch's chunks keep them bounded, see kChunkBudget). */
+struct slot {
     hipStream_t stream;
     uint8_t *dmem;
     size_t dcap;
     uint8_t *hmem;
     size_t hcap;
+};
+
+/* A host thread's resources on one device: kSlots slots, so that several
+ * chunks are in flight (copies and kernels of some while others are packed
+ * or unpacked on the host). */
+enum { kSlots = 4 };
+
+struct dctx {
+    int ready;
+    struct slot s[kSlots];
+};
+
+enum { kMaxDev = 16 };
+
+struct tctx {
+    struct dctx dev[kMaxDev];
 };
 
 static pthread_key_t tkey;
@@ -74,13 +94,18 @@ static void tctx_free(void *p)
     struct tctx *t = p;
     if (!t)
         return;
-    if (t->ready) {
-        hipSetDevice(t->device);
-        if (t->dmem)
-            hipFree(t->dmem);
-        if (t->hmem)
-            hipHostFree(t->hmem);
-        hipStreamDestroy(t->stream);
+    for (int d = 0; d < kMaxDev; d++) {
+        struct dctx *c = &t->dev[d];
+        if (!c->ready)
+            continue;
+        hipSetDevice(d);
+        for (int k = 0; k < kSlots; k++) {
+            if (c->s[k].dmem)
+                hipFree(c->s[k].dmem);
+            if (c->s[k].hmem)
+                hipHostFree(c->s[k].hmem);
+            hipStreamDestroy(c->s[k].stream);
+        }
     }
     free(t);
 }
@@ -102,17 +127,28 @@ static struct tctx *tctx_get(void)
             return NULL;
         pthread_setspecific(tkey, t);
     }
-    if (!t->ready) {
-        if (hipGetDevice(&t->device) != hipSuccess)
-            return NULL;
-        if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess)
-            return NULL;
-        t->ready = 1;
-    }
     return t;
 }
 
-static int tctx_reserve(struct tctx *t, size_t dbytes, size_t hbytes)
+/* The calling thread's context on `device`, which must be its current device. */
+static struct dctx *dctx_get(struct tctx *t, int device)
+{
+    if (device < 0 || device >= kMaxDev)
+        return NULL;
+    struct dctx *c = &t->dev[device];
+    if (!c->ready) {
+        for (int k = 0; k < kSlots; k++)
+            if (hipStreamCreateWithFlags(&c->s[k].stream, hipStreamNonBlocking) != hipSuccess) {
+                while (k-- > 0)
+                    hipStreamDestroy(c->s[k].stream);
+                return NULL;
+            }
+        c->ready = 1;
+    }
+    return c;
+}
+
+static int slot_reserve(struct slot *t, size_t dbytes, size_t hbytes)
 {
     if (dbytes > t->dcap) {
         if (t->dmem)
@@ -137,6 +173,17 @@ static int tctx_reserve(struct tctx *t, size_t dbytes, size_t hbytes)
     return 0;
 }
 
+/* The slot single calls use: slot 0 on the calling thread's current device. */
+static struct slot *single_slot(void)
+{
+    struct tctx *t = tctx_get();
+    int dev = 0;
+    if (!t || hipGetDevice(&dev) != hipSuccess)
+        return NULL;
+    struct dctx *c = dctx_get(t, dev);
+    return c ? &c->s[0] : NULL;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Device-resident batch entry points                                       */
 /* ------------------------------------------------------------------------ */
@@ -159,16 +206,34 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                                       status, nblocks, 1, s);
 }
 
-/* Scratch: the fast decoder's fallback list [count, block ids], then its
- * per-block op slots at a 256-byte boundary. */
-static size_t fallback_bytes(uint32_t nblocks)
+/* Scratch (256-byte aligned parts):
+ *   [0]     fallback count u32
+ *   [256]   op-set pool counters (LZO_MI355X_FAST_POOL_BYTES)
+ *   then    op-set return ring, u64 per set
+ *   then    the fast decoder's fallback list, u32 per block
+ *   then    the op-slot sets, one per workgroup resident at once
+ * Only the fallback list grows with nblocks (4 bytes a block). */
+enum { SCR_POOL = 256, SCR_RING = SCR_POOL + LZO_MI355X_FAST_POOL_BYTES };
+
+static size_t scr_sets(uint32_t nblocks)
 {
-    return (4 * ((size_t)nblocks + 1) + 255) & ~(size_t)255;
+    const uint32_t r = lzo_mi355x_fast_resident_blocks();
+    return nblocks < r ? nblocks : r;
+}
+
+static size_t scr_head(uint32_t nblocks)
+{
+    return ALIGN_UP(SCR_RING + 8 * scr_sets(nblocks), 256);
+}
+
+static size_t scr_ops_off(uint32_t nblocks)
+{
+    return scr_head(nblocks) + ALIGN_UP(4 * (size_t)nblocks, 256);
 }
 
 size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
 {
-    return fallback_bytes(nblocks) + (size_t)nblocks * lzo_mi355x_fast_ops_bytes_per_block();
+    return scr_ops_off(nblocks) + scr_sets(nblocks) * lzo_mi355x_fast_ops_bytes_per_block();
 }
 
 /* Fast decoder over the whole batch, then the exact decoder over the blocks
@@ -185,18 +250,22 @@ static int decompress_dev(const uint8_t *src, const uint64_t *src_off, const uin
         return 0;
     if (!scratch)
         return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
-                                                  out_len, status, NULL, nblocks, nblocks,
+                                                  out_len, status, NULL, NULL, nblocks, nblocks,
                                                   unchecked, s);
-    uint32_t *fb = (uint32_t *)scratch;
-    if (hipMemsetAsync(fb, 0, 4, s) != hipSuccess)
+    uint8_t *scr = scratch;
+    const uint32_t nsets = (uint32_t)scr_sets(nblocks);
+    uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nblocks));
+    if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)
         return -1;
     if (lzo_mi355x_launch_decompress_fast(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                          status, fb, (uint8_t *)scratch + fallback_bytes(nblocks),
-                                          nblocks, s) != 0)
+                                          status, fb, ids, (uint32_t *)(scr + SCR_POOL),
+                                          scr + SCR_RING,
+                                          scr + scr_ops_off(nblocks), nsets, nblocks, s) != 0)
         return -1;
     const uint32_t ngrid = nblocks < 512 ? nblocks : 512;
     return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
-                                              out_len, status, fb, ngrid, nblocks, unchecked, s);
+                                              out_len, status, fb, ids, ngrid, nblocks, unchecked,
+                                              s);
 }
 
 int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
@@ -298,24 +367,31 @@ void pom_copy_parallel(uint8_t *const *dst, const uint8_t *const *src, const siz
     free(jobs);
 }
 
-/* Staging layout (identical on host and device, so one copy each way):
+/* Staging layout of one chunk (identical on host and device, so one copy each
+ * way):
  *   [src_off u64][dst_off u64][src_len u32][dst_cap u32][out_len u32][status i32]
  *   [packed offset u64]
  *   [src bytes, 16-B aligned per block][dst bytes, 16-B aligned per block]
- *   [decoder scratch]  [device only: packed output]
+ *   [device only: scratch of the kernels the batch runs][device only: packed output]
  * The kernels write each block into its capacity-sized dst slot; only the
  * produced bytes come back, packed (pack kernel), in one D2H copy into the
- * host's dst region. */
+ * host's dst region.  Block i of the chunk is the caller's block ids[i]. */
 struct layout {
     size_t nb;
+    const size_t *ids;
+    int collected;          /* produced bytes packed and their D2H queued */
+    size_t packed;
     size_t o_srcoff, o_dstoff, o_srclen, o_dstcap, o_outlen, o_status, o_poff;
-    size_t o_src, o_dst, o_scr, o_pack, total, dtotal;
-    size_t src_bytes, dst_bytes;
+    size_t o_src, o_dst, o_scr, o_pack, htotal, dtotal;
 };
 
-static void layout_make(struct layout *L, size_t nb, const size_t *src_len, const size_t *dst_cap)
+static void layout_make(struct layout *L, const size_t *ids, size_t nb, const size_t *src_len,
+                        const size_t *dst_cap, int compress)
 {
     L->nb = nb;
+    L->ids = ids;
+    L->collected = 0;
+    L->packed = 0;
     size_t o = 0;
     L->o_srcoff = o; o += 8 * nb;
     L->o_dstoff = o; o += 8 * nb;
@@ -327,20 +403,18 @@ static void layout_make(struct layout *L, size_t nb, const size_t *src_len, cons
     o = ALIGN_UP(o, 256);
     L->o_src = o;
     size_t s = 0, d = 0;
-    for (size_t b = 0; b < nb; b++) {
-        s += ALIGN_UP(src_len[b], 16);
-        d += ALIGN_UP(dst_cap[b], 16);
+    for (size_t i = 0; i < nb; i++) {
+        s += ALIGN_UP(src_len[ids[i]], 16);
+        d += ALIGN_UP(dst_cap[ids[i]], 16);
     }
-    L->src_bytes = s;
-    L->dst_bytes = d;
     o += ALIGN_UP(s, 256);
     L->o_dst = o;
     o += ALIGN_UP(d, 256);
+    L->htotal = o;
     L->o_scr = o;
-    const size_t scr_d = lzo_mi355x_decompress_scratch((uint32_t)nb);
-    const size_t scr_c = lzo_mi355x_compress_scratch((uint32_t)nb);
-    o += ALIGN_UP(scr_d > scr_c ? scr_d : scr_c, 256);
-    L->total = o;
+    /* scratch of the one kernel family the batch runs */
+    o += ALIGN_UP(compress ? lzo_mi355x_compress_scratch((uint32_t)nb)
+                           : lzo_mi355x_decompress_scratch((uint32_t)nb), 256);
     L->o_pack = o;
     L->dtotal = o + ALIGN_UP(d, 256);
 }
@@ -354,15 +428,16 @@ static void layout_fill(const struct layout *L, uint8_t *h, const uint8_t *const
     uint32_t *dc = (uint32_t *)(h + L->o_dstcap);
     size_t s = 0, d = 0;
     struct copy_job *jobs = malloc(L->nb * sizeof(*jobs));
-    for (size_t b = 0; b < L->nb; b++) {
-        so[b] = s;
-        dof[b] = d;
-        sl[b] = (uint32_t)src_len[b];
-        dc[b] = (uint32_t)dst_cap[b];
+    for (size_t i = 0; i < L->nb; i++) {
+        const size_t b = L->ids[i];
+        so[i] = s;
+        dof[i] = d;
+        sl[i] = (uint32_t)src_len[b];
+        dc[i] = (uint32_t)dst_cap[b];
         if (jobs) {
-            jobs[b].dst = h + L->o_src + s;
-            jobs[b].src = src[b];
-            jobs[b].len = src_len[b];
+            jobs[i].dst = h + L->o_src + s;
+            jobs[i].src = src[b];
+            jobs[i].len = src_len[b];
         } else if (src_len[b]) {
             memcpy(h + L->o_src + s, src[b], src_len[b]);
         }
@@ -377,13 +452,48 @@ static void layout_fill(const struct layout *L, uint8_t *h, const uint8_t *const
 
 enum op_kind { OP_COMPRESS, OP_DECOMPRESS, OP_CONCAT };
 
-/* Runs one staged batch.  dst_cap: capacities used by the kernels.  On
- * return out_len/status of each block are in the pinned staging. */
-static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
+/* One host batch: the caller's arrays, the capacities the kernels use, and
+ * the plan (device split, largest-first order). */
+struct hbatch {
+    enum op_kind kind;
+    const uint8_t *const *src;
+    const size_t *src_len;
+    uint8_t *const *dst;
+    size_t *dst_len;
+    int *status;
+    const size_t *cap;
+    const size_t *cost;
+    size_t budget;
+    struct pom_plan plan;
+    const int *devs;        /* plan device d runs on HIP device devs[d] */
+    struct tctx *t;
+    uint32_t enc_lds_max;   /* chunks of at most this many blocks: LDS dictionaries */
+    int nslots;             /* chunks in flight per device (<= kSlots) */
+};
+
+/* POM_HOST_TIMING=1: per-batch and per-chunk wall times on stderr (diagnostic) */
+static int g_timing = -1;
+
+static double now_ms(void)
 {
-    uint8_t *d = t->dmem, *h = t->hmem;
-    hipStream_t s = t->stream;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+/* Chunk on slot S: inputs into pinned staging, H2D, kernels, D2H of the
+ * lengths -- all queued on the slot's stream, nothing waited for. */
+static int chunk_launch(struct slot *S, struct layout *L, const struct hbatch *B)
+{
+    if (slot_reserve(S, L->dtotal, L->htotal) != 0)
+        return -1;
+    uint8_t *d = S->dmem, *h = S->hmem;
+    hipStream_t s = S->stream;
     const uint32_t nb = (uint32_t)L->nb;
+    const double t0 = g_timing ? now_ms() : 0;
+    layout_fill(L, h, B->src, B->src_len, B->cap);
+    if (g_timing)
+        fprintf(stderr, "  chunk n=%u: fill %.2f ms (%zu B)\n", nb, now_ms() - t0, L->htotal);
     if (hipMemcpyAsync(d, h, L->o_dst, hipMemcpyHostToDevice, s) != hipSuccess)
         return -1;
     const uint8_t *dsrc = d + L->o_src;
@@ -395,59 +505,214 @@ static int run_staged(struct tctx *t, const struct layout *L, enum op_kind kind)
     uint32_t *ol = (uint32_t *)(d + L->o_outlen);
     int32_t *st = (int32_t *)(d + L->o_status);
     int rc;
-    if (kind == OP_COMPRESS)
-        rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, s);
-    else if (kind == OP_DECOMPRESS)
+    if (B->kind == OP_COMPRESS)
+        rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb,
+                                     nb <= B->enc_lds_max ? NULL : d + L->o_scr, s);
+    else if (B->kind == OP_DECOMPRESS)
         rc = decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, 0, s);
     else
         rc = lzo_mi355x_launch_decompress_concat(dsrc, so, sl, ddst, dof, dc, ol, st, nb, s);
     if (rc != 0)
         return -1;
-    if (hipMemcpyAsync(h + L->o_outlen, d + L->o_outlen, 8 * L->nb, hipMemcpyDeviceToHost, s) !=
-            hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+    return hipMemcpyAsync(h + L->o_outlen, d + L->o_outlen, 8 * L->nb, hipMemcpyDeviceToHost, s) ==
+                   hipSuccess ? 0 : -1;
+}
+
+/* Once the chunk's kernels are done (waited for, or with `poll` only if they
+ * already are), queues the pack kernel and the D2H of exactly the produced
+ * bytes.  Returns 1 when queued, 0 when polling found the kernels running,
+ * -1 on an error. */
+static int chunk_collect(struct slot *S, struct layout *L, int poll)
+{
+    if (L->collected)
+        return 1;
+    uint8_t *d = S->dmem, *h = S->hmem;
+    hipStream_t s = S->stream;
+    if (poll) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipErrorNotReady)
+            return 0;
+        if (q != hipSuccess)
+            return -1;
+    } else if (hipStreamSynchronize(s) != hipSuccess) {
         return -1;
-    /* packed offsets of the produced bytes, then one copy of exactly those */
+    }
     const uint32_t *hol = (const uint32_t *)(h + L->o_outlen);
     const uint32_t *hdc = (const uint32_t *)(h + L->o_dstcap);
     uint64_t *poff = (uint64_t *)(h + L->o_poff);
     size_t packed = 0;
-    for (size_t b = 0; b < L->nb; b++) {
-        poff[b] = packed;
-        packed += ALIGN_UP((size_t)(hol[b] < hdc[b] ? hol[b] : hdc[b]), 16);
+    for (size_t i = 0; i < L->nb; i++) {
+        poff[i] = packed;
+        packed += ALIGN_UP((size_t)(hol[i] < hdc[i] ? hol[i] : hdc[i]), 16);
     }
-    if (packed == 0)
-        return 0;
-    if (hipMemcpyAsync(d + L->o_poff, poff, 8 * L->nb, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (packed &&
+        (hipMemcpyAsync(d + L->o_poff, poff, 8 * L->nb, hipMemcpyHostToDevice, s) != hipSuccess ||
+         lzo_mi355x_launch_pack(d + L->o_dst, (const uint64_t *)(d + L->o_dstoff),
+                                (const uint32_t *)(d + L->o_outlen),
+                                (const uint32_t *)(d + L->o_dstcap),
+                                (const uint64_t *)(d + L->o_poff), d + L->o_pack,
+                                (uint32_t)L->nb, s) != 0 ||
+         hipMemcpyAsync(h + L->o_dst, d + L->o_pack, packed, hipMemcpyDeviceToHost, s) !=
+             hipSuccess))
         return -1;
-    if (lzo_mi355x_launch_pack(d + L->o_dst, dof, ol, dc, (const uint64_t *)(d + L->o_poff),
-                               d + L->o_pack, nb, s) != 0)
-        return -1;
-    if (hipMemcpyAsync(h + L->o_dst, d + L->o_pack, packed, hipMemcpyDeviceToHost, s) !=
-        hipSuccess)
-        return -1;
-    return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
+    L->packed = packed;
+    L->collected = 1;
+    return 1;
 }
 
-/* POM_HOST_TIMING=1: per-phase wall times of each host batch on stderr (diagnostic) */
-static double now_ms(void)
+/* Waits for the chunk's produced bytes and hands lengths, codes and bytes to
+ * the caller's arrays.  The next chunk (nS/nL, may be NULL) is collected
+ * first (its kernels waited for, its D2H queued), so that its copy runs
+ * while this one is unpacked.  (Polling it with hipStreamQuery instead never
+ * found it done here.) */
+static int chunk_deliver(struct slot *S, struct layout *L, const struct hbatch *B,
+                         struct slot *nS, struct layout *nL)
 {
-    struct timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+    const double t0 = g_timing ? now_ms() : 0;
+    if (chunk_collect(S, L, 0) < 0 || hipStreamSynchronize(S->stream) != hipSuccess)
+        return -1;
+    if (nS && chunk_collect(nS, nL, 0) < 0)
+        return -1;
+    const double t1 = g_timing ? now_ms() : 0;
+    const uint8_t *h = S->hmem;
+    const uint32_t *hol = (const uint32_t *)(h + L->o_outlen);
+    const int32_t *hst = (const int32_t *)(h + L->o_status);
+    const uint64_t *poff = (const uint64_t *)(h + L->o_poff);
+    struct copy_job *jobs = malloc(L->nb * sizeof(*jobs));
+    for (size_t i = 0; i < L->nb; i++) {
+        const size_t b = L->ids[i];
+        const size_t n = hol[i] < B->cap[b] ? hol[i] : B->cap[b];
+        if (jobs) {
+            jobs[i].dst = B->dst[b];
+            jobs[i].src = h + L->o_dst + poff[i];
+            jobs[i].len = n;
+        } else if (n) {
+            memcpy(B->dst[b], h + L->o_dst + poff[i], n);
+        }
+        B->dst_len[b] = hol[i];
+        B->status[b] = hst[i];
+    }
+    if (jobs) {
+        copy_jobs(jobs, L->nb);
+        free(jobs);
+    }
+    if (g_timing)
+        fprintf(stderr, "  deliver n=%zu: wait %.2f (%zu B) unpack %.2f ms\n", L->nb, t1 - t0,
+                L->packed, now_ms() - t1);
+    return 0;
+}
+
+/* A host batch is cut into chunks of at most kChunkBudget bytes of input plus
+ * output capacity (a larger block is a chunk of its own), pipelined through
+ * the device's kSlots slots: chunk k is staged and its copies and kernels are
+ * queued as soon as chunk k - kSlots has been waited for and unpacked, so the
+ * copies, the kernels of several chunks and the host-side packing overlap.
+ * The first chunk, the largest blocks, gets a quarter of the budget: their
+ * long serial LZ chains start while the rest of the batch is still being
+ * copied up.  POM_LZO_CHUNK_MB overrides the budget. */
+static const size_t kChunkBudget = (size_t)128 << 20;
+static const size_t kChunkBlocks = (size_t)1 << 20;
+/* below this many bytes per device a batch stays on one device */
+static const size_t kSplitMinBytes = (size_t)64 << 20;
+
+static int dev_run(void *arg, int d)
+{
+    const struct hbatch *B = arg;
+    const int device = B->devs[d];
+    int prev_dev = -1;
+    if (hipGetDevice(&prev_dev) != hipSuccess)
+        return -1;
+    if (prev_dev != device && hipSetDevice(device) != hipSuccess)
+        return -1;
+    int rc = 0;
+    struct dctx *c = dctx_get(B->t, device);
+    if (!c) {
+        rc = -1;
+    } else {
+        const size_t *ids = B->plan.by_dev + B->plan.dev_off[d];
+        const size_t nids = B->plan.dev_off[d + 1] - B->plan.dev_off[d];
+        struct layout L[kSlots];
+        int live[kSlots] = {0};                /* slot holds a launched chunk */
+        size_t from = 0;
+        for (int k = 0;; k++) {
+            const int cur = k % B->nslots, nxt = (k + 1) % B->nslots;
+            if (live[cur]) {                   /* chunk k - nslots: wait, unpack */
+                if (chunk_deliver(&c->s[cur], &L[cur], B, live[nxt] ? &c->s[nxt] : NULL,
+                                  &L[nxt]) != 0) {
+                    rc = -1;
+                    for (int j = 0; j < B->nslots; j++)
+                        hipStreamSynchronize(c->s[j].stream);
+                }
+                live[cur] = 0;
+            }
+            if (from < nids && rc == 0) {
+                const size_t end = pom_chunk_end(ids, from, nids, B->cost,
+                                                 k ? B->budget : B->budget / 4, kChunkBlocks);
+                layout_make(&L[cur], ids + from, end - from, B->src_len, B->cap,
+                            B->kind == OP_COMPRESS);
+                if (chunk_launch(&c->s[cur], &L[cur], B) != 0) {
+                    rc = -1;
+                    hipStreamSynchronize(c->s[cur].stream);
+                } else {
+                    live[cur] = 1;
+                }
+                from = end;
+            } else {
+                int any = 0;
+                for (int j = 0; j < B->nslots; j++)
+                    any |= live[j];
+                if (!any)
+                    break;
+            }
+        }
+    }
+    if (prev_dev != device)
+        hipSetDevice(prev_dev);
+    return rc;
+}
+
+/* Devices a host batch may use: POM_LZO_DEVICES ("0,2,3"; default every
+ * visible device).  Processes that run one rank per GPU set it to their own. */
+static int batch_devices(int *devs)
+{
+    const int count = lzo_mi355x_device_count();
+    int n = 0;
+    const char *e = getenv("POM_LZO_DEVICES");
+    if (e && *e) {
+        const char *p = e;
+        while (*p && n < kMaxDev) {
+            char *q;
+            const long v = strtol(p, &q, 10);
+            if (q == p)
+                break;
+            if (v >= 0 && v < count && v < kMaxDev)
+                devs[n++] = (int)v;
+            p = *q == ',' ? q + 1 : q;
+        }
+    } else {
+        for (int d = 0; d < count && d < kMaxDev; d++)
+            devs[n++] = d;
+    }
+    /* the caller's current device first: a one-device batch runs there */
+    int cur = -1;
+    if (n > 1 && hipGetDevice(&cur) == hipSuccess)
+        for (int i = 1; i < n; i++)
+            if (devs[i] == cur) {
+                devs[i] = devs[0];
+                devs[0] = cur;
+                break;
+            }
+    return n;
 }
 
 static int batch_common(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
                         uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks)
 {
-    static int timing = -1;
-    if (timing < 0) {
+    if (g_timing < 0) {
         const char *e = getenv("POM_HOST_TIMING");
-        timing = e && *e == '1';
+        g_timing = e && *e == '1';
     }
-    double tm[5] = {0};
-    if (timing)
-        tm[0] = now_ms();
+    const double t0 = g_timing ? now_ms() : 0;
     struct tctx *t = tctx_get();
     if (!t)
         return LZO_E_ERROR;
@@ -455,60 +720,59 @@ static int batch_common(enum op_kind kind, const uint8_t *const *src, const size
         return LZO_E_OK;
     if (nblocks > 0xFFFFFFFFu)
         return LZO_E_ERROR;
+    int devs[kMaxDev];
+    const int ndev = batch_devices(devs);
+    if (ndev <= 0)
+        return LZO_E_ERROR;
     size_t *cap = malloc(nblocks * sizeof(size_t));
-    if (!cap)
+    size_t *cost = malloc(nblocks * sizeof(size_t));
+    if (!cap || !cost) {
+        free(cap);
+        free(cost);
         return LZO_E_OUT_OF_MEMORY;
+    }
     for (size_t b = 0; b < nblocks; b++) {
         if (src_len[b] > 0xFFFFFFF0u) {
             free(cap);
+            free(cost);
             return LZO_E_ERROR;
         }
         cap[b] = kind == OP_COMPRESS ? lzo_mi355x_worst_compress(src_len[b]) : dst_len[b];
         if (cap[b] > 0xFFFFFFF0u)
             cap[b] = 0xFFFFFFF0u;
+        cost[b] = src_len[b] + cap[b];
     }
-    struct layout L;
-    layout_make(&L, nblocks, src_len, cap);
-    int rc = LZO_E_ERROR;
-    if (tctx_reserve(t, L.dtotal, L.total) == 0) {
-        if (timing)
-            tm[1] = now_ms();
-        layout_fill(&L, t->hmem, src, src_len, cap);
-        if (timing)
-            tm[2] = now_ms();
-        if (run_staged(t, &L, kind) == 0) {
-            if (timing)
-                tm[3] = now_ms();
-            const uint32_t *ol = (const uint32_t *)(t->hmem + L.o_outlen);
-            const int32_t *st = (const int32_t *)(t->hmem + L.o_status);
-            const uint64_t *poff = (const uint64_t *)(t->hmem + L.o_poff);
-            struct copy_job *jobs = malloc(nblocks * sizeof(*jobs));
-            for (size_t b = 0; b < nblocks; b++) {
-                size_t n = ol[b] < cap[b] ? ol[b] : cap[b];
-                if (jobs) {
-                    jobs[b].dst = dst[b];
-                    jobs[b].src = t->hmem + L.o_dst + poff[b];
-                    jobs[b].len = n;
-                } else if (n) {
-                    memcpy(dst[b], t->hmem + L.o_dst + poff[b], n);
-                }
-                dst_len[b] = ol[b];
-                status[b] = st[b];
-            }
-            if (jobs) {
-                copy_jobs(jobs, nblocks);
-                free(jobs);
-            }
-            rc = LZO_E_OK;
-            if (timing) {
-                tm[4] = now_ms();
-                fprintf(stderr, "pom host %s n=%zu: reserve %.2f pack %.2f gpu %.2f unpack %.2f ms\n",
-                        kind == OP_COMPRESS ? "compress" : "decompress", nblocks, tm[1] - tm[0],
-                        tm[2] - tm[1], tm[3] - tm[2], tm[4] - tm[3]);
-            }
+    struct hbatch B = {kind, src, src_len, dst, dst_len, status, cap, cost, kChunkBudget,
+                       {0, 1, NULL, NULL}, devs, t, 0, kSlots};
+    /* compress chunks that fit the LDS encoder's 4 blocks per CU at once use
+     * it: a block alone on its CU finishes twice as fast as with the
+     * dictionaries in HBM (that encoder wins only on full GPUs: 16 per CU) */
+    B.enc_lds_max = lzo_mi355x_fast_resident_blocks() / 4;
+    const char *el = getenv("POM_ENC_LDS_MAX");
+    if (el)
+        B.enc_lds_max = (uint32_t)atol(el);
+    const char *ns = getenv("POM_LZO_SLOTS");
+    if (ns && atoi(ns) >= 1 && atoi(ns) <= kSlots)
+        B.nslots = atoi(ns);
+    const char *e = getenv("POM_LZO_CHUNK_MB");
+    if (e && atol(e) > 0)
+        B.budget = (size_t)atol(e) << 20;
+    int rc = LZO_E_OUT_OF_MEMORY;
+    if (pom_plan_make(&B.plan, nblocks, cost, ndev, kSplitMinBytes) == 0) {
+        /* blocks a failed device leaves untouched read as errors */
+        for (size_t b = 0; b < nblocks; b++) {
+            status[b] = LZO_E_ERROR;
+            dst_len[b] = 0;
         }
+        rc = pom_run_devices(B.plan.ndev, dev_run, &B) == 0 ? LZO_E_OK : LZO_E_ERROR;
+        if (g_timing)
+            fprintf(stderr, "pom host %s n=%zu devices=%d: %.2f ms\n",
+                    kind == OP_COMPRESS ? "compress" : "decompress", nblocks, B.plan.ndev,
+                    now_ms() - t0);
+        pom_plan_free(&B.plan);
     }
     free(cap);
+    free(cost);
     return rc;
 }
 
@@ -587,13 +851,13 @@ enum sc_kind { SC_COMPRESS, SC_SAFE, SC_UNCHECKED };
 static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, uint8_t *dst,
                        size_t room, size_t *produced)
 {
-    struct tctx *t = tctx_get();
+    struct slot *t = single_slot();
     if (!t || src_len > 0xFFFFFFF0u || room > 0xFFFFFFF0u)
         return LZO_E_ERROR;
     const size_t o_src = SC_HDR + ALIGN_UP(room, 256);
     const size_t o_scr = o_src + ALIGN_UP(src_len, 256);
     const size_t dneed = o_scr + (kind == SC_COMPRESS ? 0 : lzo_mi355x_decompress_scratch(1));
-    if (tctx_reserve(t, dneed, o_scr) != 0)
+    if (slot_reserve(t, dneed, o_scr) != 0)
         return LZO_E_ERROR;
     uint8_t *h = t->hmem, *d = t->dmem;
     hipStream_t s = t->stream;
@@ -620,20 +884,27 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
         rc = decompress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
                             d + o_scr, 0, s);
     } else {
-        /* the unchecked decoder's own length, capped at the room (decoded
-         * again with more room when it does not fit) */
-        rc = lzo_mi355x_launch_decoded_length(d, so, sl, &dh->plen, &dh->pstatus, 1, &dh->pcap,
-                                              (uint32_t)room, s);
-        if (rc == 0)
-            rc = decompress_dev(d, so, sl, d, dof, &dh->pcap, &dh->out_len, &dh->status, 1,
-                                d + o_scr, 1, s);
+        /* decoded into the room; the unchecked decoder never reports an output
+         * overrun (lib/minilzo.c:3676-3680), so OUTPUT_OVERRUN here means the
+         * stream is longer than the room */
+        rc = decompress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
+                            d + o_scr, 1, s);
     }
     if (rc != 0 || hipMemcpyAsync(h, d, o_src, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return LZO_E_ERROR;
-    if (kind == SC_UNCHECKED && hh->plen > room) {
-        *produced = hh->plen;                      /* needs more room: the caller retries */
-        return 1;
+    if (kind == SC_UNCHECKED && hh->status == LZO_E_OUTPUT_OVERRUN) {
+        /* rare: the decoded length (input still on the GPU), then the caller
+         * retries with that much room */
+        if (lzo_mi355x_launch_decoded_length(d, so, sl, &dh->plen, &dh->pstatus, 1, NULL,
+                                             0xFFFFFFFFu, s) != 0 ||
+            hipMemcpyAsync(h, d, sizeof(*hh), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return LZO_E_ERROR;
+        if (hh->plen > room) {
+            *produced = hh->plen;
+            return 1;
+        }
     }
     const size_t n = hh->out_len < room ? hh->out_len : room;
     if (n)
@@ -671,11 +942,11 @@ int lzo1x_decompress_safe(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst,
 /* GPU pre-scan of one host-resident stream: decoded length and status. */
 int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len, unsigned long *dst_len)
 {
-    struct tctx *t = tctx_get();
+    struct slot *t = single_slot();
     if (!t || src_len > 0xFFFFFFF0u)
         return LZO_E_ERROR;
     const size_t o_src = SC_HDR;
-    if (tctx_reserve(t, o_src + src_len + 16, o_src + src_len + 16) != 0)
+    if (slot_reserve(t, o_src + src_len + 16, o_src + src_len + 16) != 0)
         return LZO_E_ERROR;
     uint8_t *h = t->hmem, *d = t->dmem;
     hipStream_t s = t->stream;
@@ -698,9 +969,9 @@ int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len, unsigne
 /* The unchecked decoder (lib/minilzo.c:3308-3699) that mds/itb.c:2964,
  * mdsl/gc.c:770 and api/api.c:6438 call.  It never learns the destination
  * size (mds/itb.c:2951-2964 passes an uninitialised *out_len): the GPU
- * pre-scans the stream's decoded length in the same launch sequence and the
- * output comes back with it; only a block that decodes to more than the
- * guessed room (16x the input, at least 256 KiB) takes a second round trip. */
+ * decodes into a guessed room (16x the input, at least 256 KiB) and the
+ * output comes back with its length in one round trip; only a block that
+ * decodes to more than that takes a length pre-scan and a second decode. */
 int lzo1x_decompress(const lzo_bytep src, lzo_uint src_len, lzo_bytep dst, lzo_uintp dst_len,
                      lzo_voidp wrkmem)
 {

@@ -34,14 +34,15 @@ int lzo_mi355x_launch_compress(const uint8_t *src, const uint64_t *src_off,
 
 /* Exact (grammar-serial) decoder, lzo1x_decompress_safe semantics, or with
  * `unchecked` those of the unchecked lzo1x_decompress.  fb NULL: grid entry b
- * decodes block b (ngrid = nblocks).  Otherwise the fb[0] blocks listed at
- * fb[1..] are decoded by a grid of ngrid workgroups. */
+ * decodes block b (ngrid = nblocks).  Otherwise the *fb blocks listed at
+ * fb_ids[] are decoded by a grid of ngrid workgroups. */
 int lzo_mi355x_launch_decompress_exact(const uint8_t *src, const uint64_t *src_off,
                                        const uint32_t *src_len, uint8_t *dst,
                                        const uint64_t *dst_off, const uint32_t *dst_cap,
                                        uint32_t *out_len, int32_t *status,
-                                       const uint32_t *fb, uint32_t ngrid,
-                                       uint32_t nblocks, int unchecked, hipStream_t stream);
+                                       const uint32_t *fb, const uint32_t *fb_ids,
+                                       uint32_t ngrid, uint32_t nblocks, int unchecked,
+                                       hipStream_t stream);
 
 /* Exact decoder over blocks of consecutive streams (the hvfs_fwritev column
  * layout): each stream decodes with lzo1x_decompress_safe semantics right
@@ -53,16 +54,22 @@ int lzo_mi355x_launch_decompress_concat(const uint8_t *src, const uint64_t *src_
                                         hipStream_t stream);
 
 /* Throughput decoder (lzo1x_decode_fast.hip).  Blocks it does not finish
- * exactly are appended to fb (fb[0] = count, must be 0 on entry) and get
- * status 0x7FFF0001 until the exact decoder runs on them.  ops: device
- * scratch of nblocks * lzo_mi355x_fast_ops_bytes_per_block() bytes (the
- * parser wave's op slots). */
+ * exactly are appended to fallback_ids[] (*fallback = count, must be 0 on
+ * entry) and get status 0x7FFF0001 until the exact decoder runs on them.
+ * ops: nsets op-slot sets of lzo_mi355x_fast_ops_bytes_per_block() bytes,
+ * shared by the workgroups through a pool (pool: LZO_MI355X_FAST_POOL_BYTES
+ * of counters, ring: nsets u64, all zero on entry); nsets = min(nblocks,
+ * lzo_mi355x_fast_resident_blocks()) keeps every resident workgroup busy. */
+#define LZO_MI355X_FAST_POOL_BYTES 8192
 size_t lzo_mi355x_fast_ops_bytes_per_block(void);
+uint32_t lzo_mi355x_fast_resident_blocks(void);
 int lzo_mi355x_launch_decompress_fast(const uint8_t *src, const uint64_t *src_off,
                                       const uint32_t *src_len, uint8_t *dst,
                                       const uint64_t *dst_off, const uint32_t *dst_cap,
-                                      uint32_t *out_len, int32_t *status, uint32_t *fb,
-                                      void *ops, uint32_t nblocks, hipStream_t stream);
+                                      uint32_t *out_len, int32_t *status, uint32_t *fallback,
+                                      uint32_t *fallback_ids, uint32_t *pool, void *ring,
+                                      void *ops, uint32_t nsets, uint32_t nblocks,
+                                      hipStream_t stream);
 
 /* Unchecked-decoder pre-scan: decoded length and status per block; with
  * cap_out, also min(length, cap_limit) per block (a decode's capacity). */

@@ -32,25 +32,32 @@ lzo.compress_dev(src, zb, zl, zs); torch.cuda.synchronize()
 zsrc = lzo.DeviceBatch(za, zb.off, zl)
 out = torch.zeros_like(src.arena); ob = lzo.DeviceBatch(out, src.off, src.length)
 ol = torch.zeros_like(zl); os_ = torch.zeros_like(zl)
-fb = torch.zeros(nb + 1, dtype=torch.int32, device=dev)
+head = torch.zeros(64 + 2048, dtype=torch.int32, device=dev)   # fallback count, op-set pool
+fb = head[:1]
+ids = torch.zeros(nb, dtype=torch.int32, device=dev)
+lib.lzo_mi355x_fast_resident_blocks.restype = ctypes.c_uint32
+nsets = min(nb, int(lib.lzo_mi355x_fast_resident_blocks()))
+ring = torch.zeros(nsets, dtype=torch.int64, device=dev)
 lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
-opsbuf = torch.empty(nb * lib.lzo_mi355x_fast_ops_bytes_per_block(), dtype=torch.uint8, device=dev)
+opsbuf = torch.empty(nsets * lib.lzo_mi355x_fast_ops_bytes_per_block(), dtype=torch.uint8, device=dev)
 SLOTS = 40
 stamps = torch.zeros(nb * SLOTS, dtype=torch.int64, device=dev)
 fn = lib.lzo_mi355x_debug_decompress_fast_stamps
 fn.restype = ctypes.c_int
-fn.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+fn.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 fast = lib.lzo_mi355x_launch_decompress_fast
 fast.restype = ctypes.c_int
-fast.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
+fast.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
 p = lambda x: x.data_ptr()
 sh = torch.cuda.current_stream().cuda_stream
 def run(stamp):
-    fb.zero_()
+    head.zero_(); ring.zero_()
+    args = (p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_),
+            p(head), p(ids), p(head) + 256, p(ring), p(opsbuf), nsets, nb)
     if stamp:
-        fn(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), p(opsbuf), nb, p(stamps), sh)
+        fn(*args, p(stamps), sh)
     else:
-        fast(p(zsrc.arena), p(zsrc.off), p(zsrc.length), p(out), p(ob.off), p(ob.length), p(ol), p(os_), p(fb), p(opsbuf), nb, sh)
+        fast(*args, sh)
 for stamp in ((False,) if a.nostamps else (False, True)):
     run(stamp); torch.cuda.synchronize()
     ts = []
@@ -64,7 +71,7 @@ for stamp in ((False,) if a.nostamps else (False, True)):
         olr = ol.cpu().numpy().astype(np.uint32)
         fbb = np.nonzero((olr >> 16) == 0xFA11)[0]
         print("  fast-path refusals (block, reason):", [(int(x), int(olr[x] & 15)) for x in fbb[:8]])
-        per = opsbuf.numel() // nb
+        per = opsbuf.numel() // nsets   # (op-set contents; the set a block used is not recorded)
         for x in fbb[:4]:
             blk = opsbuf[int(x) * per: (int(x) + 1) * per].cpu().numpy()
             zs_ = za[int(zb.off[int(x)].item()): int(zb.off[int(x)].item()) + int(zl[int(x)].item())].cpu().numpy()
@@ -92,11 +99,12 @@ rsf = stamps.view(nb, SLOTS)[:, len(phases) + counts.index("reason")].cpu().nump
 rs = (rsf & 15).astype(int)
 for b in np.nonzero(rs)[0][:4]:
     q, w0 = int((rsf[b] >> 4) & 0xFFFFFFF), int(rsf[b] >> 32)
-    per = opsbuf.numel() // nb
+    per = opsbuf.numel() // nsets   # (op-set contents; the set a block used is not recorded)
     slot = opsbuf[b * per: (b + 1) * per].view(torch.int32).view(-1, 2).cpu().numpy()
     kslots = 8
     ops_q = slot[(q % kslots) * (len(slot) // kslots): (q % kslots + 1) * (len(slot) // kslots)]
     np.save(os.path.join(ROOT, "gpurun_out", f"refused_b{b}_q{q}.npy"), ops_q)
     print("refused block", int(b), "reason", int(rs[b]), "piece", q, "window", w0)
-names = ["none", "off_end", "bad", "ops", "dead", "ewait", "overrun", "lookbehind", "space", "landed", "head"]
+names = ["none", "off_end", "bad", "ops", "dead", "ewait", "overrun", "lookbehind", "space", "landed", "head",
+         "writer"]
 print("refusals:", {names[r]: int((rs == r).sum()) for r in np.unique(rs) if r})

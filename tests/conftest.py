@@ -21,7 +21,8 @@ def pytest_configure(config):
 def _ensure_built():
     need = [os.path.join(ROOT, "pomegranate_amd", "liblzo_mi355x.so"),
             os.path.join(ROOT, "pomegranate_amd", "libpom_synth.so"),
-            os.path.join(ROOT, "oracle", "liboracle.so")]
+            os.path.join(ROOT, "oracle", "liboracle.so"),
+            os.path.join(ROOT, "tests", "native", "libsplit_mock.so")]
     if not all(os.path.exists(p) for p in need):
         import __graft_entry__
         __graft_entry__.build()

@@ -274,6 +274,26 @@ def test_fast_path_takes_every_valid_stream(dev, gu):
     assert fallbacks == 0
 
 
+def test_fast_path_op_sets_are_reused(dev, gu):
+    """More blocks than workgroups resident at once: the op-slot sets are
+    handed from finished workgroups to new ones (the scratch holds one set per
+    resident workgroup, not per block), every block stays on the fast path,
+    and the scratch for config C4's 131,072 blocks stays well under 300 MB."""
+    lib = lzo.load()
+    resident = int(lib.lzo_mi355x_fast_resident_blocks())
+    n = 2 * resident + 123
+    blocks = [synth.block(synth.ITB, 70000 + i, 4096 + 16 * (i % 64)) for i in range(n)]
+    comps, st = gu.gpu_compress(torch, blocks, dev)
+    assert all(s == 0 for s in st)
+    outs, st2, fallbacks = gu.gpu_decompress_fast(torch, comps, [len(b) for b in blocks], dev)
+    assert all(s == 0 for s in st2)
+    assert outs == blocks
+    assert fallbacks == 0
+    assert lzo.decompress_scratch_bytes(131072) < 300e6
+    assert lzo.decompress_scratch_bytes(n) == lzo.decompress_scratch_bytes(resident) + (
+        -(-4 * n // 256) - -(-4 * resident // 256)) * 256
+
+
 def _mutated_streams(oracle, count=192, seed=23):
     """Valid ITB streams with the damage real storage or wire errors do: a few
     flipped bytes, a truncation, trailing garbage, a zeroed run."""
