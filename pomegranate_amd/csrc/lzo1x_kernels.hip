@@ -24,7 +24,6 @@ namespace {
 constexpr int kWave = 64;
 
 constexpr int E_OK = 0;
-constexpr int E_ERROR = -1;
 constexpr int E_INPUT_OVERRUN = -4;
 constexpr int E_OUTPUT_OVERRUN = -5;
 constexpr int E_LOOKBEHIND_OVERRUN = -6;
@@ -427,11 +426,18 @@ __global__ __launch_bounds__(kWave) void lzo1x_decode_concat_kernel(
 // matching lane ends the window, and the writes of the lanes before it are
 // committed in position order with ds_max.
 //   dict word: [31:25] claiming lane (0x7F = none), [24:0] position+1 (0 = EMPTY)
+// Positions are relative to `base`, which moves up 16 MiB at a time: every
+// entry that old is past the largest match distance (0xBFFF) by then, so the
+// rebase turns it EMPTY -- which the probe treats exactly like a stale entry
+// (lib/minilzo.c:2944-2960 goes to `literal` either way) -- and shifts the
+// others down.  Blocks of any length thus fit 25-bit positions.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSlots = emit::kSlots;
 constexpr uint32_t kPosMask = (1u << 25) - 1;
 constexpr uint32_t kNoClaim = 0x7Fu << 25;
 constexpr uint32_t kStage = 8192;
+constexpr uint32_t kRebase = 1u << 24;             // base step (positions stay below 2^25 - 1)
+static_assert(kRebase + 0xC000u + 64u < kPosMask, "relative positions fit the dict word");
 using emit::Enc;
 using emit::slot_primary;
 using emit::slot_secondary;
@@ -443,9 +449,18 @@ __device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
     const uint8_t* in = e.in;
     const uint32_t n = e.n;
     const uint32_t ip_end = n - 13;                // lib/minilzo.c:2929
-    uint32_t ip = 4, ii = 0;
+    uint32_t ip = 4, ii = 0, base = 0;
 
     for (;;) {
+        while (ip - base >= kRebase + 0xC000u) {   // entries below base + kRebase are stale
+            // (a loop: one long match can move ip on by many steps)
+            for (uint32_t s = l; s < kSlots; s += kWave) {
+                const uint32_t v = dict[s] & kPosMask;
+                dict[s] = kNoClaim | (v > kRebase ? v - kRebase : 0u);
+            }
+            wave_order();
+            base += kRebase;
+        }
         const uint32_t p = ip + l;
         const bool active = l == 0 || p < ip_end;
         uint32_t h1 = 0, h2 = 0, w1 = 0, w2 = 0, b3 = 0, b0 = 0, b1 = 0, b2 = 0;
@@ -485,9 +500,9 @@ __device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
         bool ok = false;
         uint32_t slot = h1, cand = 0;
         if (l < navail) {
-            const uint32_t c1 = (w1 & kPosMask) - 1;
+            const uint32_t c1 = base + (w1 & kPosMask) - 1;
             const bool v1 = (w1 & kPosMask) != 0 && p - c1 <= 0xBFFFu;
-            const uint32_t c2 = (w2 & kPosMask) - 1;
+            const uint32_t c2 = base + (w2 & kPosMask) - 1;
             const bool v2 = (w2 & kPosMask) != 0 && p - c2 <= 0xBFFFu;
             if (v1) {
                 if (p - c1 <= 0x800u || in[c1 + 3] == b3) {
@@ -507,7 +522,7 @@ __device__ uint32_t enc_parse(Enc& e, uint32_t* dict)
         const uint64_t mm = wave_ballot(ok);
         const uint32_t ndone = mm ? ctz64(mm) + 1 : navail;
         if (l < ndone)     // UPDATE_I in position order
-            atomicMax(&dict[slot], kNoClaim | (p + 1));
+            atomicMax(&dict[slot], kNoClaim | (p - base + 1));
         wave_order();
 
         if (!mm) {
@@ -572,14 +587,6 @@ __global__ __launch_bounds__(kWave) void lzo1x_encode_kernel(
     e.smask = kStage - 1;
     e.sflush = kStage / 2;
     e.op = e.flushed = 0;
-    if (e.n > kPosMask - 1) {                      // positions must fit 25 bits
-        if (l == 0) {
-            out_len[b] = 0;
-            status[b] = E_ERROR;
-        }
-        return;
-    }
-
     uint32_t t;
     if (e.n <= 13) {                               // lib/minilzo.c:3167-3168
         t = e.n;

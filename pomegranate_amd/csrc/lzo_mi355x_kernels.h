@@ -24,7 +24,7 @@ int lzo_mi355x_launch_compress_fast(const uint8_t *src, const uint64_t *src_off,
                                     uint32_t *out_len, int32_t *status, uint32_t nblocks,
                                     void *scratch, size_t scratch_bytes, hipStream_t stream);
 
-/* General encoder (lzo1x_kernels.hip), any block size below 32 MiB.
+/* General encoder (lzo1x_kernels.hip), any block size.
  * pending_only: only blocks whose status is LZO_MI355X_ENC_PENDING. */
 int lzo_mi355x_launch_compress(const uint8_t *src, const uint64_t *src_off,
                                const uint32_t *src_len, uint8_t *dst,

@@ -352,7 +352,7 @@ def _large_block(n, seed):
     return b"".join(parts)[:n]
 
 
-@pytest.mark.parametrize("n", [(3 << 20) + 5, 16 << 20, (16 << 20) + 1])
+@pytest.mark.parametrize("n", [(3 << 20) + 5, 16 << 20, (16 << 20) + 1, (32 << 20) + 5])
 def test_large_blocks_vs_oracle(dev, gu, oracle, n):
     """Blocks up to the throughput encoder's 16 MiB limit and one byte past it
     (the general encoder), byte-identical to the oracle, and decoded back."""
@@ -361,6 +361,26 @@ def test_large_blocks_vs_oracle(dev, gu, oracle, n):
     assert st == [0]
     assert comps[0] == oracle.compress(blk)
     outs, st2, _ = gu.gpu_decompress(torch, comps, [n], dev)
+    assert st2 == [0] and outs[0] == blk
+
+
+def test_blocks_past_32_mib_vs_oracle(dev, gu, oracle):
+    """The general encoder keeps 25-bit dictionary positions relative to a
+    base that moves up 16 MiB at a time; blocks of any length stay
+    byte-identical to the oracle (the reference handles any length).  The
+    block repeats 13 MiB of random bytes three times (every earlier copy is
+    past the 0xBFFF match distance, so the reference finds no match there:
+    a stale entry must never pass for a live one after a rebase), then has a
+    20 MiB zero run (one match moves ip over several rebase steps) and
+    ITB-like data."""
+    rng = np.random.default_rng(32)
+    period = rng.integers(0, 256, (13 << 20) + 7, dtype=np.uint8).tobytes()
+    blk = period * 3 + bytes(20 << 20) + synth.block(synth.ITB, 33, 2 << 20)
+    assert len(blk) > 60 << 20
+    comps, st = gu.gpu_compress(torch, [blk], dev)
+    assert st == [0]
+    assert comps[0] == oracle.compress(blk)
+    outs, st2, _ = gu.gpu_decompress(torch, comps, [len(blk)], dev)
     assert st2 == [0] and outs[0] == blk
 
 

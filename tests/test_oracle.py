@@ -9,6 +9,7 @@ from __future__ import annotations
 import hashlib
 import random
 
+import numpy as np
 import pytest
 
 from conftest import batch_sizes
@@ -127,3 +128,12 @@ def test_generated_full_grammar_streams(oracle, ref_lib):
         z, out = lzo_streams.stream(seed, [50, 300, 5000, 40000][seed % 4])
         assert oracle.decompress_safe(z, len(out)) == (0, out), seed
         assert ref_lib.decompress_safe(z, len(out)) == (0, out), seed
+
+
+def test_oracle_matches_reference_past_32_mib(oracle, ref_lib):
+    """The oracle's encoder on a block past 32 MiB (the general GPU encoder's
+    rebased positions are checked against it) equals lib/minilzo.c itself."""
+    rng = np.random.default_rng(32)
+    period = rng.integers(0, 256, (13 << 20) + 7, dtype=np.uint8).tobytes()
+    blk = period * 3 + bytes(20 << 20) + synth.block(synth.ITB, 33, 2 << 20)
+    assert oracle.compress(blk) == ref_lib.compress(blk)
