@@ -701,6 +701,10 @@ def main():
     backend = os.environ.get("POM_DIST_BACKEND", "nccl")
     dev = torch.device(f"cuda:{local % torch.cuda.device_count()}")
     torch.cuda.set_device(dev)
+    # One rank per GPU: the library's host batches stay on this rank's GPU
+    # (its own split over every visible GPU is for single-process callers).
+    if world > 1:
+        os.environ.setdefault("POM_LZO_DEVICES", str(dev.index))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":

@@ -879,3 +879,23 @@ extern "C" int lzo_mi355x_debug_compress_fast_stamps(const uint8_t* src, const u
                        stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Diagnostic: the global-dictionary encoder with parse-wave phase stamps.
+extern "C" int lzo_mi355x_debug_compress_gdict_stamps(const uint8_t* src, const uint64_t* src_off,
+                                                      const uint32_t* src_len, uint8_t* dst,
+                                                      const uint64_t* dst_off,
+                                                      const uint32_t* dst_cap, uint32_t* out_len,
+                                                      int32_t* status, uint32_t nblocks,
+                                                      void* scratch, size_t scratch_bytes,
+                                                      uint64_t* stamps, hipStream_t stream)
+{
+    uint32_t grid = (uint32_t)(scratch_bytes / kDictBytes);
+    grid = grid < nblocks ? grid : nblocks;
+    grid = grid < enc_resident() ? grid : enc_resident();
+    if (grid == 0)
+        return -1;
+    hipLaunchKernelGGL(lzo1x_encode_gdict_kernel<true>, dim3(grid), dim3(2 * kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
+                       (uint8_t*)scratch, stamps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

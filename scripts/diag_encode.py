@@ -34,26 +34,35 @@ fn = getattr(lib, "lzo_mi355x_debug_compress_fast_stamps", None)
 if fn is not None:
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p] * 8 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+gfn = getattr(lib, "lzo_mi355x_debug_compress_gdict_stamps", None)
+if gfn is not None:
+    gfn.restype = ctypes.c_int
+    gfn.argtypes = [ctypes.c_void_p] * 8 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.c_void_p, ctypes.c_void_p]
 p = lambda x: x.data_ptr()
 sh = torch.cuda.current_stream().cuda_stream
 scr = torch.empty(max(lzo.compress_scratch_bytes(nb), 1), dtype=torch.uint8, device=dev)
 ref_out = None
-for mode in ("lds", "gdict", "stamps"):
-    if mode == "stamps" and (fn is None or a.nostamps):
+gstamps = torch.zeros(nb * SLOTS, dtype=torch.int64, device=dev)
+for mode in ("lds", "gdict", "stamps", "gstamps"):
+    if mode in ("stamps", "gstamps") and (fn is None or gfn is None or a.nostamps):
         continue
     ts = []
-    for _ in range(1 if mode == "stamps" else 5):
+    for _ in range(1 if mode in ("stamps", "gstamps") else 5):
         za.zero_()
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
         if mode == "stamps":
             fn(p(src.arena), p(src.off), p(src.length), p(za), p(zb.off), p(zb.length), p(zl), p(zs), nb, p(stamps), sh)
+        elif mode == "gstamps":
+            gfn(p(src.arena), p(src.off), p(src.length), p(za), p(zb.off), p(zb.length), p(zl), p(zs), nb,
+                p(scr), scr.numel(), p(gstamps), sh)
         else:
             lzo.compress_dev(src, zb, zl, zs, scratch=scr if mode == "gdict" else None)
         e1.record(); torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     same = ""
-    if mode != "stamps":
+    if mode not in ("stamps", "gstamps"):
         got = (za.clone(), zl.clone())
         if ref_out is None:
             ref_out = got
@@ -62,9 +71,10 @@ for mode in ("lds", "gdict", "stamps"):
     print(f"{mode}: {float(np.median(ts)):.3f} ms (min {min(ts):.3f}), status ok {bool((zs == 0).all())}{same}")
 if fn is None or a.nostamps:
     sys.exit(0)
-st = stamps.view(nb, SLOTS).double().cpu().numpy()
 phases = ["setup", "probe", "cand", "path", "claim", "tok", "dict", "pushwait"]
 counts = ["windows", "extend", "tokens", "pathit", "extit", "end_cross", "end_cap", "fwd"]
-print("parse cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases)},
-      "total", int(st[:, :len(phases)].sum(1).mean()))
-print("counts/block (mean):", {n: round(float(st[:, len(phases) + i].mean()), 1) for i, n in enumerate(counts)})
+for name, t_ in (("lds", stamps), ("gdict", gstamps)):
+    st = t_.view(nb, SLOTS).double().cpu().numpy()
+    print(name, "parse cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases)},
+          "total", int(st[:, :len(phases)].sum(1).mean()))
+    print(name, "counts/block (mean):", {n: round(float(st[:, len(phases) + i].mean()), 1) for i, n in enumerate(counts)})

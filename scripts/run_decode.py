@@ -1,5 +1,7 @@
-"""Decode-only driver for profiling: the bench workload (4096 x 64 KiB ITB
-blocks), compressed once on the GPU, then decoded --reps times."""
+"""Driver for profiling one kernel family on the bench workload (4096 x 64 KiB
+ITB blocks): --op decode (default) compresses once on the GPU, then decodes
+--reps times; --op encode compresses --reps times (with the dictionary
+scratch, as bench.py does), then checks one decode."""
 import argparse, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -14,6 +16,7 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--model", default="itb")
 ap.add_argument("--lib", default=None, help="alternative liblzo_mi355x.so build")
 ap.add_argument("--noverify", action="store_true", help="exit 0 even if the output differs (timing variants)")
+ap.add_argument("--op", choices=("decode", "encode"), default="decode")
 a = ap.parse_args()
 if a.lib:
     lzo.LIB_PATH = a.lib
@@ -28,15 +31,17 @@ zo = np.zeros(nb, dtype=np.uint64); zo[1:] = np.cumsum((caps[:-1].astype(np.uint
 za = torch.zeros(int(zo[-1]) + int(caps[-1]) + 256, dtype=torch.uint8, device=dev)
 zb = lzo.DeviceBatch(za, t(zo.view(np.int64)), t(caps.view(np.int32)))
 zl = torch.zeros(nb, dtype=torch.int32, device=dev); zs = torch.zeros_like(zl)
-lzo.compress_dev(src, zb, zl, zs); torch.cuda.synchronize()
+for _ in range(a.reps if a.op == "encode" else 1):
+    lzo.compress_dev(src, zb, zl, zs)
+torch.cuda.synchronize()
 zsrc = lzo.DeviceBatch(za, zb.off, zl)
 out = torch.zeros_like(src.arena); ob = lzo.DeviceBatch(out, src.off, src.length)
 ol = torch.zeros_like(zl); st = torch.zeros_like(zl)
 scr = torch.empty(lzo.decompress_scratch_bytes(nb), dtype=torch.uint8, device=dev)
-for _ in range(a.reps):
+for _ in range(a.reps if a.op == "decode" else 1):
     lzo.decompress_dev(zsrc, ob, ol, st, scr)
 torch.cuda.synchronize()
 ok = torch.equal(out, src.arena) and bool((st == 0).all())
 print({"blocks": nb, "n_bytes": int(lens.astype(np.int64).sum()), "z_bytes": int(zl.long().sum()),
-       "reps": a.reps, "ok": ok}, flush=True)
+       "reps": a.reps, "op": a.op, "ok": ok}, flush=True)
 sys.exit(0 if ok or a.noverify else 1)
