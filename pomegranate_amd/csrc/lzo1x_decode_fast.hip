@@ -126,7 +126,7 @@ constexpr uint32_t kInfoErr = 1u << 17;          // piece info: the block needs 
 constexpr uint32_t kStepSpan = 16 * kWave + 16;
 // (diagnostics: why, in bits 20..23 of the piece info / the CN_REASON stamp)
 enum { RS_NONE, RS_OFF_END, RS_BAD, RS_OPS, RS_DEAD, RS_EWAIT, RS_OVERRUN, RS_LOOKBEHIND,
-       RS_SPACE, RS_LANDED, RS_HEAD, RS_WRITER };
+       RS_SPACE, RS_LANDED, RS_HEAD, RS_WRITER, RS_POOL };
 
 // parse states (instruction starts)
 constexpr uint32_t ST_A = 0;   // top: t < 16 is a literal run
@@ -1247,7 +1247,8 @@ __device__ __forceinline__ void src_commit(FastLds& S, uint32_t l, const SrcCopy
 //   return: j = ret_p++; that ring entry for j = {j + 1, set}.
 // A workgroup waits only while every set of its partition is held by a
 // running workgroup (resident, so it finishes): no deadlock, whatever the
-// occupancy or dispatch order.
+// occupancy or dispatch order.  (The wait is still bounded: after ~1 s the
+// block goes to the exact decoder, which needs no op slots.)
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPoolParts = 32;
 constexpr uint32_t kPoolStride = 64;             // u32 words per partition (256 B: two 128-B lines)
@@ -1265,6 +1266,8 @@ __device__ __forceinline__ uint32_t pool_parts(uint32_t nsets)
     return nsets < kPoolParts ? nsets : kPoolParts;
 }
 
+constexpr uint32_t kNoSet = 0xFFFFFFFFu;
+
 __device__ uint32_t opset_take(const OpPool& P, uint32_t b)
 {
     const uint32_t parts = pool_parts(P.nsets), p = b % parts;
@@ -1275,13 +1278,14 @@ __device__ uint32_t opset_take(const OpPool& P, uint32_t b)
     const uint32_t j = i - count;
     const unsigned long long want = (unsigned long long)(j + 1) << 32;
     unsigned long long* const e = &P.ring[p + (j % count) * parts];
-    for (;;) {
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
         // relaxed: only the set number passes (an acquire would invalidate the L2)
         const unsigned long long v = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((v & ~0xFFFFFFFFull) == want)
             return (uint32_t)v;
         __builtin_amdgcn_s_sleep(8);
     }
+    return kNoSet;
 }
 
 __device__ void opset_return(const OpPool& P, uint32_t set)
@@ -1319,7 +1323,8 @@ __device__ void block_close(FastLds& S, uint32_t b, uint32_t* __restrict__ out_l
         const uint32_t at = atomicAdd(&fallback[0], 1u);
         fallback_ids[at] = b;
     }
-    opset_return(P, S.opset);
+    if (S.opset != kNoSet)
+        opset_return(P, S.opset);
 }
 
 template <bool STAMPS>
@@ -1373,12 +1378,13 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     k.cap = dst_cap[b];
     k.P = 0;
     k.staged = 0;
-    uint2* const gops = ops + (size_t)__builtin_amdgcn_readfirstlane(S.opset) * (kSlots * kOpMax);
+    const uint32_t opset = __builtin_amdgcn_readfirstlane(S.opset);
+    uint2* const gops = ops + (size_t)(opset == kNoSet ? 0u : opset) * (kSlots * kOpMax);
 
     // The exact decoder takes: destinations not 16-byte aligned, empty or huge
     // blocks (lengths up to 255 * z must not wrap 32 bits).
-    bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0;
-    uint32_t reason = refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
+    bool refuse = ((uintptr_t)k.out & 15) != 0 || k.z >= (1u << 24) || k.z == 0 || opset == kNoSet;
+    uint32_t reason = opset == kNoSet ? (uint32_t)RS_POOL : refuse ? (uint32_t)RS_HEAD : (uint32_t)RS_NONE;
     if (wave == 1) {
         if (POM_PRIO && last_round)
             __builtin_amdgcn_s_setprio(POM_PARSER_PRIO);

@@ -10,7 +10,7 @@ for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   out=gpurun_out/encvar/lib_$name.so
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C -Iinclude $flags -c $C/lzo1x_encode_fast.hip -o /tmp/encf_$name.o || exit 1
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $C/lzo1x_kernels.o /tmp/encf_$name.o $C/lzo1x_decode_fast.o $C/lzo_host.o $C/itb_codec.o $C/column_codec.o $C/xnet_frame.o -Wl,-Bsymbolic -lpthread || exit 1
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $C/lzo1x_kernels.o /tmp/encf_$name.o $C/lzo1x_decode_fast.o $C/lzo_host.o $C/batch_split.o $C/itb_codec.o $C/column_codec.o $C/xnet_frame.o -Wl,-Bsymbolic -lpthread || exit 1
   echo "== $name ($flags)"
   timeout -k 10 200 python scripts/diag_encode.py --lib $out 2>&1 | grep -E "stamps=False|kernel" | head -3 || exit 1
 done

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 1
 C=pomegranate_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C -Iinclude -DPOM_EXEC_SKIP=1 -c $C/lzo1x_decode_fast.hip -o /tmp/ponly.o || exit 1
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o gpurun_out/lib_ponly.so $C/lzo1x_kernels.o $C/lzo1x_encode_fast.o /tmp/ponly.o $C/lzo_host.o $C/itb_codec.o $C/column_codec.o $C/xnet_frame.o -Wl,-Bsymbolic -lpthread || exit 1
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o gpurun_out/lib_ponly.so $C/lzo1x_kernels.o $C/lzo1x_encode_fast.o /tmp/ponly.o $C/lzo_host.o $C/batch_split.o $C/itb_codec.o $C/column_codec.o $C/xnet_frame.o -Wl,-Bsymbolic -lpthread || exit 1
 export TMPDIR=/tmp
 for v in full ponly; do
   lib=""; [ $v = ponly ] && lib="--lib gpurun_out/lib_ponly.so"

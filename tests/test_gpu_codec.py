@@ -294,6 +294,42 @@ def test_fast_path_op_sets_are_reused(dev, gu):
         -(-4 * n // 256) - -(-4 * resident // 256)) * 256
 
 
+@pytest.mark.parametrize("nsets", [1, 3, 40])
+def test_fast_path_op_set_pool_under_contention(dev, gu, nsets):
+    """The op-set pool with far fewer sets than blocks (the library sizes it to
+    the resident workgroups; here the launcher gets 1, 3 or 40 sets for 600
+    blocks): workgroups wait for sets returned by finished ones, in every
+    partition, and each block still decodes exactly on the fast path."""
+    import ctypes
+    lib = lzo.load()
+    fn = lib.lzo_mi355x_launch_decompress_fast
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
+    n = 600
+    blocks = [synth.block(synth.ITB, 80000 + i, 4096 + 64 * (i % 97)) for i in range(n)]
+    comps, st = gu.gpu_compress(torch, blocks, dev)
+    assert all(x == 0 for x in st)
+    src = gu.device_batch(torch, comps, dev)
+    dst = gu.empty_batch(torch, [len(b) for b in blocks], dev, fill=0x5A)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    ost = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    head = torch.zeros(64 + 2048, dtype=torch.int32, device=dev)   # fallback count + pool counters
+    ids = torch.zeros(n, dtype=torch.int32, device=dev)
+    ring = torch.zeros(nsets, dtype=torch.int64, device=dev)
+    ops = torch.empty(nsets * lib.lzo_mi355x_fast_ops_bytes_per_block(), dtype=torch.uint8,
+                      device=dev)
+    p = lambda t: t.data_ptr()
+    rc = fn(p(src.arena), p(src.off), p(src.length), p(dst.arena), p(dst.off), p(dst.length),
+            p(olen), p(ost), p(head), p(ids), p(head) + 256, p(ring), p(ops), nsets, n,
+            torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert int(head[0].item()) == 0                       # no block left the fast path
+    assert ost.cpu().numpy().tolist() == [0] * n
+    assert gu.fetch(dst, olen) == blocks
+
+
 def _mutated_streams(oracle, count=192, seed=23):
     """Valid ITB streams with the damage real storage or wire errors do: a few
     flipped bytes, a truncation, trailing garbage, a zeroed run."""
