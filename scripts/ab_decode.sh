@@ -1,5 +1,7 @@
 #!/bin/bash
-# A/B decoder variants (scripts/variants.sh specs), each diag run REPS times.
+# A/B decoder variants: each "NAME:FLAGS" spec builds liblzo_mi355x.so with the
+# decoder compiled with FLAGS, then runs scripts/diag_decode.py REPS times.
+# Usage (on the GPU box): REPS=3 bash scripts/ab_decode.sh "base:" "v1:-DPOM_SLOTS=8"
 set -u
 REPS=${REPS:-3}
 mkdir -p gpurun_out/variants
