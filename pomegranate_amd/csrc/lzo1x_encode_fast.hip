@@ -543,47 +543,34 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
 }
 
 // ---------------------------------------------------------------------------
-// Emit wave
+// Emitter: tokens -> the LZO1X byte stream (lzo1x_emit.h) in an LDS ring,
+// stored to HBM.  Run by the emit wave (two-wave kernels) or, in the fused
+// kernel, by the parse wave itself after each window.
 // ---------------------------------------------------------------------------
 template <bool GD>
-__device__ void emit_wave(EncLdsT<GD>& S, const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap,
-                          uint32_t* out_len, int32_t* status, uint32_t b)
-{
+struct Emitter {
+    EncLdsT<GD>& S;
     emit::Enc e;
-    e.in = in;
-    e.n = n;
-    e.out = out;
-    e.cap = cap;
-    e.stage = S.stage;
-    e.smask = kStage - 1;
-    e.sflush = kStage / 2;
-    e.op = e.flushed = 0;
-    uint32_t ct = 0;                                 // tokens consumed
-    uint32_t pos = 0;                                // input covered by the tokens so far
-    bool poisoned = false;                           // a token the parse cannot have meant
-    // Lines ahead of the parse wave go to L2 from this wave, so the parse
-    // wave's probe, candidate and extension loads hit there: one dword per
-    // 128-B line, 8 KiB per load instruction; waiting on them stalls only
-    // this wave.
-    const uintptr_t lines = (uintptr_t)in & ~(uintptr_t)127;
-    const uintptr_t last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
-    uint32_t pf = 0;                                 // bytes from `lines` already touched
-    auto prefetch = [&]() {
-        if (!POM_ENC_AHEAD)
-            return;
-        const uint32_t ahead = *(volatile uint32_t*)&S.ip + POM_ENC_AHEAD;
-        const uint32_t want = ahead < n + 127 ? ahead : n + 127;
-        if (pf >= want)
-            return;
-        uint32_t x = 0;
-        for (; pf < want; pf += 128 * kWave) {
-            const uintptr_t a = lines + pf + 128 * lane_id();
-            if (a <= last)
-                x ^= *(gdword*)a;
-        }
-        if (x == 0x9E3779B9u)                        // (keeps the loads; never matters)
-            S.sink = x;
-    };
+    BlockSrc B;
+    uint32_t n;
+    uint32_t ct;                                     // tokens consumed
+    uint32_t pos;                                    // input covered by the tokens so far
+    bool poisoned;                                   // a token the parse cannot have meant
+
+    __device__ __forceinline__ Emitter(EncLdsT<GD>& S_, const uint8_t* in, uint32_t n_, uint8_t* out,
+                                       uint32_t cap)
+        : S(S_), B(block_src(in, n_)), n(n_), ct(0), pos(0), poisoned(false)
+    {
+        e.in = in;
+        e.n = n_;
+        e.out = out;
+        e.cap = cap;
+        e.stage = S_.stage;
+        e.smask = kStage - 1;
+        e.sflush = kStage / 2;
+        e.op = e.flushed = 0;
+    }
+
     // Lane-parallel emission of the pending tokens, lane k writing token
     // ct + k: the byte offsets are a prefix sum of the token sizes, a short
     // literal run's length goes into the previous match's second-to-last
@@ -593,9 +580,9 @@ __device__ void emit_wave(EncLdsT<GD>& S, const uint8_t* in, uint32_t n, uint8_t
     // than kLitMax literals, needs extension zeros, fails the checks below,
     // or would overrun the ring; that token takes the one-at-a-time path.
     // Returns the number of tokens written.
-    constexpr uint32_t kLitMax = 16;
-    const BlockSrc B = block_src(in, n);
-    auto emit_batch = [&](uint32_t prod) -> uint32_t {
+    static constexpr uint32_t kLitMax = 16;
+    __device__ uint32_t batch(uint32_t prod)
+    {
         const uint32_t k = lane_id();
         const uint32_t avail = prod - ct < (uint32_t)kWave ? prod - ct : (uint32_t)kWave;
         const uint4 t = S.tok[(ct + (k < avail ? k : 0u)) % kTok];
@@ -681,18 +668,16 @@ __device__ void emit_wave(EncLdsT<GD>& S, const uint8_t* in, uint32_t n, uint8_t
         pos += lane_read(iadv, nb - 1);
         emit::maybe_flush(e);
         return nb;
-    };
-    for (;;) {
-        prefetch();
-        const uint32_t prod = lds_load(&S.prod);
-        if (ct == prod) {
-            __builtin_amdgcn_s_sleep(POM_EMIT_SLEEP);
-            continue;
-        }
+    }
+
+    // Emits the tokens up to prod.  Returns true once the tail token (the
+    // block's last) is written, with out_len[b] and status[b] set.
+    __device__ bool drain(uint32_t prod, uint32_t* out_len, int32_t* status, uint32_t b)
+    {
         while (ct < prod) {
 #ifndef POM_ENC_NOEMIT
             if (POM_ENC_BATCH && !poisoned) {
-                const uint32_t nb = emit_batch(prod);
+                const uint32_t nb = batch(prod);
                 if (nb) {
                     ct += nb;
                     lds_store(&S.cons, ct);
@@ -717,7 +702,7 @@ __device__ void emit_wave(EncLdsT<GD>& S, const uint8_t* in, uint32_t n, uint8_t
                     status[b] = poisoned || t.y != n - pos ? -1          // LZO_E_ERROR
                               : e.op <= e.cap ? 0 : -5;  // LZO_E_OK / LZO_E_OUTPUT_OVERRUN
                 }
-                return;
+                return true;
             }
 #ifdef POM_ENC_NOEMIT
             if (POM_ENC_NOEMIT) {                    // (timing experiment only: no output)
@@ -737,6 +722,49 @@ __device__ void emit_wave(EncLdsT<GD>& S, const uint8_t* in, uint32_t n, uint8_t
             }
             lds_store(&S.cons, ct);
         }
+        return false;
+    }
+};
+
+// Emit wave (two-wave kernels): drains the token queue as the parse wave
+// fills it.
+template <bool GD>
+__device__ void emit_wave(EncLdsT<GD>& S, const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap,
+                          uint32_t* out_len, int32_t* status, uint32_t b)
+{
+    Emitter<GD> E(S, in, n, out, cap);
+    // Lines ahead of the parse wave go to L2 from this wave, so the parse
+    // wave's probe, candidate and extension loads hit there: one dword per
+    // 128-B line, 8 KiB per load instruction; waiting on them stalls only
+    // this wave.
+    const uintptr_t lines = (uintptr_t)in & ~(uintptr_t)127;
+    const uintptr_t last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
+    uint32_t pf = 0;                                 // bytes from `lines` already touched
+    auto prefetch = [&]() {
+        if (!POM_ENC_AHEAD)
+            return;
+        const uint32_t ahead = *(volatile uint32_t*)&S.ip + POM_ENC_AHEAD;
+        const uint32_t want = ahead < n + 127 ? ahead : n + 127;
+        if (pf >= want)
+            return;
+        uint32_t x = 0;
+        for (; pf < want; pf += 128 * kWave) {
+            const uintptr_t a = lines + pf + 128 * lane_id();
+            if (a <= last)
+                x ^= *(gdword*)a;
+        }
+        if (x == 0x9E3779B9u)                        // (keeps the loads; never matters)
+            S.sink = x;
+    };
+    for (;;) {
+        prefetch();
+        const uint32_t prod = lds_load(&S.prod);
+        if (E.ct == prod) {
+            __builtin_amdgcn_s_sleep(POM_EMIT_SLEEP);
+            continue;
+        }
+        if (E.drain(prod, out_len, status, b))
+            return;
     }
 }
 
