@@ -45,28 +45,38 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
+    """A rank: its round-robin share through the library's planner with a
+    stand-in for the codec (tests/native/split_mock.c: output = input
+    reversed), then the completion barrier."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        import sys
-        sys.path.insert(0, os.path.join(os.path.dirname(__file__)))
-        from conftest import Oracle
-        oracle = Oracle()
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(os.path.dirname(__file__), "native", "libsplit_mock.so"))
+        lib.mock_batch.restype = ctypes.c_int
         nglobal = 64
         mine = shard.round_robin(nglobal, rank, world)
         arena, offs, lens = synth.batch(synth.ITB, 0, [16384] * len(mine), seeds=mine)
-        h = hashlib.sha256()
-        errors = 0
-        for b in range(len(mine)):
-            d = arena[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
-            z = oracle.compress(d)
-            rc, back = oracle.decompress_safe(z, len(d))
-            errors += int(rc != 0 or back != d)
-            h.update(z)
+        blocks = [arena[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+                  for b in range(len(mine))]
+        n = len(blocks)
+        srcs = [ctypes.create_string_buffer(b, len(b)) for b in blocks]
+        dsts = [ctypes.create_string_buffer(len(b)) for b in blocks]
+        vp = lambda bufs: (ctypes.c_void_p * n)(*[ctypes.addressof(x) for x in bufs])
+        ln = (ctypes.c_size_t * n)(*[len(b) for b in blocks])
+        dev_of = (ctypes.c_int * n)()
+        chunk_of = (ctypes.c_long * n)()
+        seq_of = (ctypes.c_long * n)()
+        used = ctypes.c_int(0)
+        rc = lib.mock_batch(ctypes.c_size_t(n), vp(srcs), ln, vp(dsts), 2, ctypes.c_size_t(1 << 16),
+                            ctypes.c_size_t(1 << 17), ctypes.c_size_t(1 << 20), dev_of, chunk_of,
+                            seq_of, ctypes.byref(used))
+        errors = int(rc != 0) + sum(int(d.raw != b[::-1]) for d, b in zip(dsts, blocks))
+        h = hashlib.sha256(b"".join(blocks)).hexdigest()
         errors_all, elapsed = shard.completion_barrier(dist, torch.device("cpu"), errors,
                                                        0.5 + rank)
-        q.put((rank, mine, errors_all, elapsed, h.hexdigest()))
+        q.put((rank, mine, errors_all, elapsed, h))
     finally:
         dist.destroy_process_group()
 
@@ -86,3 +96,50 @@ def test_two_rank_gloo_completion_barrier():
     assert sorted(ids0 + ids1) == list(range(64))
     assert e0 == e1 == 0                       # summed over ranks
     assert t0 == t1 == pytest.approx(1.5)      # max over ranks
+
+
+def _gpu_worker(rank, world, port, q):
+    """A rank on the GPU box: its share through the real library (host
+    batches on cuda:0, both ranks sharing the one GPU), checked by round trip;
+    the compressed bytes go back to the parent, which checks them against the
+    oracle."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["POM_LZO_DEVICES"] = "0"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from pomegranate_amd import lzo
+        mine = shard.round_robin(48, rank, world)
+        blocks = [synth.block(synth.ITB, 7000 + i, 4096 + 1024 * (i % 13)) for i in mine]
+        rc, st, comps = lzo.compress_batch(blocks)
+        rc2, st2, outs = lzo.decompress_batch(comps, [len(b) for b in blocks])
+        errors = int(rc != 0 or rc2 != 0) + sum(int(x != 0) for x in st + st2) + \
+            sum(int(o != b) for o, b in zip(outs, blocks))
+        errors_all, elapsed = shard.completion_barrier(dist, torch.device("cpu"), errors, 1.0)
+        q.put((rank, mine, errors_all, comps))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_share_the_gpu_codec(oracle):
+    """The N>1 bench path in rehearsal with the real GPU codec: two gloo ranks
+    (one GPU box), round-robin shares, completion barrier; every compressed
+    block equals the oracle's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=120) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(res[0][1] + res[1][1]) == list(range(48))
+    assert res[0][2] == res[1][2] == 0
+    for rank, mine, _, comps in res:
+        for i, z in zip(mine, comps):
+            assert z == oracle.compress(synth.block(synth.ITB, 7000 + i, 4096 + 1024 * (i % 13)))
