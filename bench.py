@@ -540,7 +540,7 @@ def _c5_xnet(args, recs, originals, tmps, rbufs, path, itb, xnet, plain_bytes):
         af.close()
         t1 = time.perf_counter()
         fd = os.open(path, os.O_RDONLY)
-        stored = [itb.read_record(fd, loc, out=b) for loc, b in zip(locs, rbufs)]
+        stored = itb.read_batch(fd, locs, rbufs)
         os.close(fd)
         ta = time.perf_counter()
         rc2, wl2 = xnet.reply_batch(stored, reqs, 0x200, 3, wire)
@@ -592,7 +592,7 @@ def run_c5(args, rank):
             af.close()
             t2 = time.perf_counter()
             fd = os.open(path, os.O_RDONLY)
-            back = [itb.read_record(fd, loc, out=b) for loc, b in zip(locs, rbufs)]
+            back = itb.read_batch(fd, locs, rbufs)            # pom_itb_read_batch
             os.close(fd)
             t3 = time.perf_counter()
             comp_idx = [i for i, b in enumerate(back) if itb.header_fields(b)[2] == itb.COMPR_LZO]

@@ -14,7 +14,8 @@
  *                                   and its twin       mdsl/gc.c:755-786
  *   pom_abuf_*                   <- append_buf_write / append_buf_flush_remap
  *                                   mdsl/storage.c:384-519 (ITB append file)
- *   pom_itb_read                 <- the header-then-payload ITB read of the
+ *   pom_itb_read, pom_itb_read_batch
+ *                                <- the header-then-payload ITB read of the
  *                                   MDSL read path (mdsl/storage.c:2507-2640)
  */
 #ifndef POM_ITB_H
@@ -84,6 +85,13 @@ int pom_abuf_close(struct pom_abuf *ab);
 /* Reads the ITB record at `location` of fd: the 264-byte header first, then
  * the rest of h.len.  *len = h.len.  -EINVAL: h.len < 264 or > cap. */
 int pom_itb_read(int fd, uint64_t location, uint8_t *buf, size_t cap, size_t *len);
+
+/* pom_itb_read of n records (an MDSL batch of ITB loads), split over up to 8
+ * threads: record i from locations[i] into buf[i] (capacity cap[i]); len[i]
+ * and err[i] (0 or the -errno pom_itb_read returns) per record.  Returns 0,
+ * or -ENOMEM. */
+int pom_itb_read_batch(int fd, const uint64_t *locations, size_t n, uint8_t *const *buf,
+                       const size_t *cap, size_t *len, int *err);
 
 #ifdef __cplusplus
 }

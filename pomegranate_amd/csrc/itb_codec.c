@@ -13,6 +13,7 @@
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <pthread.h>
 #include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
@@ -334,5 +335,48 @@ int pom_itb_read(int fd, uint64_t location, uint8_t *buf, size_t cap, size_t *le
     if (rc)
         return rc;
     *len = l;
+    return 0;
+}
+
+struct read_range {
+    int fd;
+    const uint64_t *loc;
+    uint8_t *const *buf;
+    const size_t *cap;
+    size_t *len;
+    int *err;
+    size_t lo, hi;
+};
+
+static void *read_worker(void *arg)
+{
+    const struct read_range *r = arg;
+    for (size_t i = r->lo; i < r->hi; i++) {
+        r->len[i] = 0;
+        r->err[i] = pom_itb_read(r->fd, r->loc[i], r->buf[i], r->cap[i], &r->len[i]);
+    }
+    return NULL;
+}
+
+int pom_itb_read_batch(int fd, const uint64_t *locations, size_t n, uint8_t *const *buf,
+                       const size_t *cap, size_t *len, int *err)
+{
+    enum { kReadThreads = 8 };
+    const size_t nt = n >= 64 ? kReadThreads : 1;
+    struct read_range r[kReadThreads];
+    pthread_t th[kReadThreads];
+    int started[kReadThreads] = {0};
+    for (size_t k = 0; k < nt; k++) {
+        r[k] = (struct read_range){fd, locations, buf, cap, len, err, n * k / nt, n * (k + 1) / nt};
+        if (k > 0)
+            started[k] = pthread_create(&th[k], NULL, read_worker, &r[k]) == 0;
+    }
+    read_worker(&r[0]);
+    for (size_t k = 1; k < nt; k++) {
+        if (started[k])
+            pthread_join(th[k], NULL);
+        else
+            read_worker(&r[k]);
+    }
     return 0;
 }

@@ -53,6 +53,8 @@ def _lib() -> ctypes.CDLL:
         lib.pom_itb_read.restype = ctypes.c_int
         lib.pom_itb_read.argtypes = [ctypes.c_int, ctypes.c_uint64, _vp, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_size_t)]
+        lib.pom_itb_read_batch.restype = ctypes.c_int
+        lib.pom_itb_read_batch.argtypes = [ctypes.c_int, _vp, ctypes.c_size_t, _vp, _vp, _vp, _vp]
         _bound = True
     return lib
 
@@ -175,6 +177,28 @@ class AppendFile:
         rc = self.lib.pom_abuf_close(ctypes.byref(self.ab))
         if rc:
             raise OSError(-rc, os.strerror(-rc))
+
+
+def read_batch(fd: int, locations, outs) -> list:
+    """pom_itb_read_batch: record i at locations[i] into outs[i] (writable
+    buffers, len = cap), read on up to 8 threads.  Returns outs; raises
+    OSError for the first record that failed."""
+    lib = _lib()
+    n = len(locations)
+    loc = (ctypes.c_uint64 * max(n, 1))(*locations)
+    keep = [(ctypes.c_char * len(o)).from_buffer(o) for o in outs]
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(c) for c in keep])
+    caps = (ctypes.c_size_t * max(n, 1))(*[len(o) for o in outs])
+    lens = (ctypes.c_size_t * max(n, 1))()
+    errs = (ctypes.c_int * max(n, 1))()
+    rc = lib.pom_itb_read_batch(fd, loc, n, ptrs, caps, lens, errs)
+    del keep
+    if rc:
+        raise OSError(-rc, os.strerror(-rc))
+    for i in range(n):
+        if errs[i]:
+            raise OSError(-errs[i], f"record {i}: " + os.strerror(-errs[i]))
+    return list(outs)
 
 
 def read_record(fd: int, location: int, cap: int = ITB_FULL,

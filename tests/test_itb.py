@@ -73,6 +73,28 @@ def test_append_batch_matches_single_appends(tmp_path, win):
     assert open(batch, "rb").read() == open(single, "rb").read()
 
 
+def test_read_batch_matches_single_reads(tmp_path):
+    """pom_itb_read_batch (8 threads) reads what pom_itb_read reads, record by
+    record, and reports a record whose header does not fit its buffer."""
+    import os
+    recs = _records(150, seed=8)
+    path = str(tmp_path / "itbs")
+    a = itb.AppendFile(path)
+    locs = a.append_batch(recs, [itb.header_fields(r)[0] for r in recs])
+    a.close()
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        single = [bytes(itb.read_record(fd, loc)) for loc in locs]
+        outs = itb.read_batch(fd, locs, [bytearray(itb.ITB_FULL) for _ in locs])
+        assert [bytes(o) for o in outs] == single
+        small = [bytearray(itb.ITB_FULL) for _ in locs[:70]]
+        small[66] = bytearray(300)                       # h.len > cap: -EINVAL
+        with pytest.raises(OSError, match="record 66"):
+            itb.read_batch(fd, locs[:70], small)
+    finally:
+        os.close(fd)
+
+
 def _expected_compress(oracle, rec):
     """itb_lzo_compress, restated: returns (which, expected oi record bytes)."""
     ln = itb.header_fields(rec)[0]
