@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include "lzo_mi355x.h"
@@ -211,15 +212,12 @@ int pom_abuf_append(struct pom_abuf *ab, const void *rec, size_t len, uint64_t *
     return 0;
 }
 
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23
-#endif
-
 /* A batch of appends with the locations of n single appends in order.  Each
- * window's share is pre-faulted in one madvise (page-by-page write faults on
- * the shared mapping were the append's main cost) and copied by the threaded
- * copier; a full window is unmapped and the next mapped as in
- * pom_abuf_append. */
+ * window's share goes to the file in one gathered write (pwritev); a full
+ * window is unmapped and the next mapped as in pom_abuf_append, so single and
+ * batched appends interleave freely.  (Pre-faulting the window with
+ * MADV_POPULATE_WRITE and copying on 8 threads took twice as long.) */
+enum { kIovMax = 1024 };
 int pom_abuf_append_batch(struct pom_abuf *ab, const void *const *recs, const size_t *lens,
                           size_t n, uint64_t *locations)
 {
@@ -234,7 +232,6 @@ int pom_abuf_append_batch(struct pom_abuf *ab, const void *const *recs, const si
         free(len);
         return -ENOMEM;
     }
-    const size_t page = (size_t)sysconf(_SC_PAGESIZE);
     int rc = 0;
     size_t b = 0, done = 0;         /* record b, bytes of it already placed */
     while (b < n && !rc) {
@@ -267,9 +264,41 @@ int pom_abuf_append_batch(struct pom_abuf *ab, const void *const *recs, const si
         if (rc)
             break;
         if (off > start) {
-            const size_t p0 = start / page * page;
-            (void)madvise(ab->addr + p0, off - p0, MADV_POPULATE_WRITE);   /* best effort */
-            pom_copy_parallel(dst, src, len, nj);
+            /* one gathered write of the window's share into the page cache the
+             * window maps (coherent on Linux): about twice as fast as faulting
+             * the window's pages in and copying (C5 write), same file */
+            struct iovec iov[kIovMax];
+            uint64_t fo = ab->file_offset + start;
+            for (size_t j0 = 0; j0 < nj && !rc; j0 += kIovMax) {
+                const size_t m = nj - j0 < kIovMax ? nj - j0 : kIovMax;
+                size_t want = 0;
+                for (size_t j = 0; j < m; j++) {
+                    iov[j].iov_base = (void *)src[j0 + j];
+                    iov[j].iov_len = len[j0 + j];
+                    want += len[j0 + j];
+                }
+                size_t got = 0;
+                while (got < want) {                 /* (a short write resumes) */
+                    struct iovec *v = iov;
+                    size_t nv = m, skip = got;
+                    while (skip >= v->iov_len) {
+                        skip -= v->iov_len;
+                        v++;
+                        nv--;
+                    }
+                    v->iov_base = (uint8_t *)v->iov_base + skip;
+                    v->iov_len -= skip;
+                    const ssize_t w = pwritev(ab->fd, v, (int)nv, (off_t)(fo + got));
+                    if (w <= 0) {
+                        rc = w < 0 ? -errno : -EIO;
+                        break;
+                    }
+                    got += (size_t)w;
+                }
+                fo += want;
+            }
+            if (rc)
+                break;
         }
         ab->offset = off;
         if (ab->offset >= ab->win) {
