@@ -404,6 +404,24 @@ def timed(torch, dist, world, stream, phases, steps, warmup):
     return wall, per
 
 
+def copy_gbps(torch, dev, nbytes=1 << 30, reps=10):
+    """Measured HBM bandwidth of a plain device-to-device copy (read + write
+    bytes per second), SURVEY.md §8(d): reported next to the 8 TB/s peak."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    for _ in range(2):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / reps
+    del a, b
+    return 2 * nbytes / t / 1e9
+
+
 def roofline(kind, nbytes, kernel_s, block_bytes, nblocks, note):
     """HBM roofline of one kernel: algorithmic bytes (compressed + uncompressed,
     SURVEY.md §8(d)) per launch over the launch's average duration."""
@@ -498,6 +516,10 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
         "errors": errors,
         "fallback_blocks": R.fallback_blocks,
     }
+    copy = copy_gbps(torch, dev)
+    for key in ("roofline", "compress_roofline"):
+        result[key]["copy_GBps_measured"] = round(copy, 1)
+        result[key]["frac_of_copy"] = round(result[key]["achieved"] / copy, 4)
     if world == 1 and args.workload in ("c2", "c3"):
         # Successive decode batches on two streams (each launch's 4096 blocks
         # fill the chip in one round, so its first pieces and last blocks

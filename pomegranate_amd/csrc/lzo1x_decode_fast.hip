@@ -184,6 +184,11 @@ __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ void wave_order() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+// Lane masks straight from a v_cmp (a ballot of a compound bool costs a
+// v_cndmask and a v_cmp more): active lanes with a < b, a >= b, (int)a >= 0.
+__device__ __forceinline__ uint64_t mask_lt(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 36); }
+__device__ __forceinline__ uint64_t mask_ge(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 35); }
+__device__ __forceinline__ uint64_t mask_nonneg(uint32_t a) { return __builtin_amdgcn_sicmp((int32_t)a, 0, 39); }
 
 // Inclusive prefix sum over the wave: DPP row shifts inside each 16-lane row,
 // then the row totals via readlane (no LDS round trip).
@@ -1566,8 +1571,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             uint32_t s = 0;
             while (s < nwin) {
                 const uint32_t os = lane_read(o, s);
-                const bool brk = l > s && outsrc && send > os;
-                const uint64_t bm = wave_ballot(brk);
+                // lanes l > s reading output at or after os (send is 0 unless outsrc)
+                const uint64_t bm = mask_lt(os, send) & (~1ull << s);
                 const uint32_t e = bm ? (uint32_t)__builtin_ctzll(bm) : nwin;
                 const uint32_t c_beg = lane_read(cs, s);
                 const uint32_t c_end = e < nwin ? lane_read(cs, e) : wchunks;
@@ -1641,18 +1646,26 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     const bool two = p >= 16u && n1 < len;      // the chunk wraps the period
                     const uint32_t aA = small ? bb : bb + r0;
                     const uint32_t aB = bb + r0 - p;            // wrapped part, read p lower
-                    const uint64_t smask = wave_ballot(live && small);
+                    const uint64_t mlive = mask_lt(c, c_end);
+                    const uint64_t mtwo = mask_ge(p, 16u) & mask_lt(n1, len);
+                    const uint64_t smask = mlive & mask_lt(p - 1u, 15u);
                     const uint32_t ps = small ? p * 32u + r0 : 0u;   // selectors of the expansion
                     // LDS: the ring (its mirror takes reads across the end) or
                     // the linear source buffer; HBM: literals beyond the buffer,
                     // output below the ring (a + kRing < xs: those slots were
                     // overwritten before this step)
-                    const bool hA = live && (lin ? aA >= kLinHbm : aA + kRing < xs);
-                    const bool hB = live && two && (lin ? aB >= kLinHbm : bb + kRing < xs);
+                    // (as signed distances, without branches: lin -> a - kLinHbm >= 0,
+                    // else xs - kRing - 1 - a >= 0)
+                    const uint32_t hbase = lin ? kLinHbm : 0u, hlim = lin ? 0u : xs - kRing - 1u;
+                    const uint32_t kA = lin ? aA - hbase : hlim - aA, kB = lin ? aB - hbase : hlim - bb;
+                    const bool hA = live && (int32_t)kA >= 0;
+                    const bool hB = live && two && (int32_t)kB >= 0;
+                    const uint64_t mhbm = mlive & (mask_nonneg(kA) | (mtwo & mask_nonneg(kB)));
                     const uint32_t amask = lin ? kLdsMask : kRingMask;
-                    // only the reads some lane of the step needs (uniform branches)
-                    uint4 vA, vB = make_uint4(0, 0, 0, 0), sl = vB, sh = vB;
-                    const bool any_two = wave_ballot(two) != 0;
+                    // only the reads some lane of the step needs (uniform branches;
+                    // vB / sl / sh are read only on the paths that load them)
+                    uint4 vA, vB, sl, sh;
+                    const bool any_two = mtwo != 0;
                     const uint32_t ra = base + (live ? aA & amask : 0u);
                     if (!smask) {
                         if (!any_two)
@@ -1665,8 +1678,8 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         lds_read16x4(ra, base + (two ? aB & amask : 0u), psel0 + ps, psel1 + ps, vA, vB, sl,
                                      sh);
                     }
-                    if (wave_ballot(hA || hB)) {
-                        if (wave_ballot((hA || hB) && !lin) && xs + 16u > kRing)
+                    if (mhbm) {
+                        if ((mhbm & mask_nonneg(op.y)) && xs + 16u > kRing)   // (!lin: bit 31 clear)
                             landed_seen = wait_landed(S, xs + 16u - kRing, landed_seen, refuse);
                         const uint8_t* gb = lin ? k.in - kLinHbm : k.out;
                         if (hA)
@@ -1705,7 +1718,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         if (xd < 16u)                  // keep the mirror of ring[0, 16)
                             lds_write_part(base + kRing + xd, v, len);
                     }
-                    if (wave_ballot(wcross)) {
+                    if (mask_lt(kRing, xd + len)) {     // (wcross; len is 0 off the step)
                         if (wcross) {                  // destination wraps the ring end
                             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
                             uint8_t* ldsw = (uint8_t*)&S;

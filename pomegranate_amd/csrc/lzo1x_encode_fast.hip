@@ -28,6 +28,7 @@
 //    an LDS ring and stores it to HBM, off the parse wave's critical path.
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <stdint.h>
 
 #include "lzo_mi355x_kernels.h"
@@ -148,6 +149,11 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v)
 }
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __ballot(p); }
+// Lane masks straight from a v_cmp (a ballot of a compound bool costs a
+// v_cndmask and a v_cmp more): active lanes with a == b, a < b, a >= b.
+__device__ __forceinline__ uint64_t mask_eq(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 32); }
+__device__ __forceinline__ uint64_t mask_lt(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 36); }
+__device__ __forceinline__ uint64_t mask_ge(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 35); }
 __device__ __forceinline__ void wave_order() { emit::order(); }
 
 __device__ __forceinline__ uint32_t lds_load(const uint32_t* p)
@@ -248,301 +254,6 @@ __device__ uint32_t extend_match(const BlockSrc& B, uint32_t n, uint32_t mc, uin
 }
 
 // ---------------------------------------------------------------------------
-// Parse wave
-// ---------------------------------------------------------------------------
-// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums and counts of
-// the parse wave go to stamps[b * kEncStampSlots + i]; no output depends on them.
-enum { EP_SETUP, EP_PROBE, EP_CAND, EP_PATH, EP_CLAIM, EP_TOK, EP_DICT, EP_PUSHWAIT,
-       EC_WINDOWS, EC_EXTEND, EC_TOKENS, EC_PATHIT, EC_EXTIT, EC_C2NEED, EC_C2MATCH, EC_FWD, EP_N };
-constexpr int kEncStampSlots = 16;
-
-template <bool STAMPS, bool GD>
-__device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, uint32_t n, uint32_t l,
-                           uint64_t* acc)
-{
-    uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-#define ESTAMP(ph)                                                  \
-    do {                                                            \
-        if (STAMPS) {                                               \
-            const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
-            acc[ph] += now_ - tmark;                                \
-            tmark = now_;                                           \
-        }                                                           \
-    } while (0)
-    uint32_t tp = 0;                                // tokens produced
-    uint32_t cons_seen = 0;
-    auto push = [&](uint32_t from, uint32_t nlit, uint32_t mlen, uint32_t off) {
-        if (STAMPS)
-            acc[EC_TOKENS] += 1;
-        ESTAMP(EP_TOK);
-        while (tp - cons_seen >= kTok) {             // the emit wave always drains
-            __builtin_amdgcn_s_sleep(2);
-            cons_seen = lds_load(&S.cons);
-        }
-        ESTAMP(EP_PUSHWAIT);
-        if (l == 0)
-            S.tok[tp % kTok] = make_uint4(from, nlit, mlen, off);
-        tp++;
-        lds_store(&S.prod, tp);
-    };
-
-    const BlockSrc B = block_src(in, n);
-    uint32_t ii = 0;                                // first byte not yet emitted
-    if (n > 13) {                                   // lib/minilzo.c:3167-3173
-        for (uint32_t s = l; s < kSlots / 2; s += kWave)
-            D.put2(s, 0);                           // zero-filled wrkmem: all EMPTY
-        for (uint32_t s = l; s < kClaim; s += kWave)
-            S.claim[s] = 0xFFFFFFFFu;               // (tag 0xFFFFFF: no window has it)
-        if (GD)
-            __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0): the table is zero in L2
-        wave_order();
-        const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
-        uint32_t ip = 4;
-        uint32_t base = 0;                          // dictionary position base
-        uint32_t wtag = 0xFFFFFEu;                  // claim tag of the window (one per window, > 0)
-        // Probe words of the window (position ip + l): the next window's are
-        // read as soon as its start is known, ahead of the token and
-        // dictionary writes.
-        uint32_t pw[kCmpW];
-        load_at<kCmpW>(B, ip + l, pw);
-        ESTAMP(EP_SETUP);
-        for (;;) {
-            if (STAMPS)
-                acc[EC_WINDOWS] += 1;
-            if (ip + kWave - base >= 0xFFFFu) {     // this window's positions would not fit
-                const uint32_t nb = (ip - (kM4MaxOffset + 1)) / kRebase * kRebase;
-                const uint32_t delta = nb - base;
-                for (uint32_t s2 = l; s2 < kSlots / 2; s2 += kWave) {
-                    const uint32_t pr = D.get2(s2);
-                    const uint32_t lo = pr & 0xFFFFu, hi = pr >> 16;
-                    const uint32_t nlo = lo > delta ? lo - delta : 0u;
-                    const uint32_t nhi = hi > delta ? hi - delta : 0u;
-                    D.put2(s2, nlo | (nhi << 16));
-                }
-                if (GD)
-                    __builtin_amdgcn_s_waitcnt(0x0F70);
-                wave_order();
-                base = nb;
-            }
-            if (POM_ENC_AHEAD)
-                S.ip = ip;
-            const uint32_t p = ip + l;
-            const bool active = l == 0 || p < ip_end;   // the first probe always runs
-            // (every lane probes; an inactive one ends with no candidate)
-            const uint32_t h1 = emit::slot_primary(pw[0] & 0xFF, (pw[0] >> 8) & 0xFF,
-                                                   (pw[0] >> 16) & 0xFF, pw[0] >> 24);
-            const uint32_t h2 = emit::slot_secondary(h1);
-            const uint32_t e1 = D.get(h1), e2 = D.get(h2);
-            const uint32_t w1 = active && e1 ? base + e1 - 1 : 0u;   // (positions >= 4: 0 stays "empty")
-            const uint32_t w2 = active && e2 ? base + e2 - 1 : 0u;
-            const uint64_t am = wave_ballot(active);
-            const uint32_t nact = (uint32_t)__builtin_popcountll(am);
-            if (STAMPS)
-                __builtin_amdgcn_s_waitcnt(0);       // (attribute the probe loads here)
-            ESTAMP(EP_PROBE);
-
-            // Probe decision of every active lane with the pre-window
-            // dictionary, lib/minilzo.c:2940-2971 (exact up to the cut below).
-            const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
-            const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
-            uint32_t c1w[kCmpW], c2w[kCmpW];        // (read unconditionally; used only if valid)
-            load_at<kCmpW>(B, w1, c1w);
-            load_at<kCmpW>(B, w2, c2w);
-            const uint32_t b3 = pw[0] >> 24;
-            // (selects, no branches)
-            const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
-            bool use2 = v1 && !c1pass;               // the secondary slot is read and written
-            const bool c2pass = use2 && v2 && (p - w2 <= kM2MaxOffset || (c2w[0] >> 24) == b3);
-            const bool tm = c1pass || c2pass;
-            uint32_t slot = use2 ? h2 : h1, cand = c2pass ? w2 : w1;
-            uint32_t cw[kCmpW];
-#pragma unroll
-            for (int i = 0; i < kCmpW; i++)
-                cw[i] = c2pass ? c2w[i] : c1w[i];
-            // try_match (:2962-2971), then the match length as far as kCmpB bytes
-            bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
-            uint32_t mlen = first_diff<kCmpW>(cw, pw);
-            mlen = mlen < n - p ? mlen : n - p;
-
-            // ---- the greedy path through the window, speculatively ----------
-            // From lane 0: a matching lane jumps over its match, any other
-            // lane is a literal.  Lanes inside matches neither probe nor
-            // update the dictionary (:3051-3150).
-            uint64_t okm = wave_ballot(ok);
-            if (STAMPS) {
-                __builtin_amdgcn_s_waitcnt(0);       // (attribute the candidate loads here)
-                acc[EC_C2NEED] += 0;
-                acc[EC_C2MATCH] += 0;
-            }
-            ESTAMP(EP_CAND);
-            uint64_t path = 0, mstart = 0;
-            uint32_t end = 0;                        // lane where the path leaves the window
-            uint32_t nmatch = 0;
-            // the path from lane `from` on (lanes below it stay as they are)
-            auto walk = [&](uint32_t from) {
-                end = from;
-                while (end < nact) {
-                    if (STAMPS)
-                        acc[EC_PATHIT] += 1;
-                    const uint64_t rest = okm & (~0ull << end);
-                    const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
-                    const uint32_t lit_end = q < nact ? q : nact;
-                    if (lit_end > end)               // literal lanes end .. lit_end-1
-                        path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
-                    if (q >= nact) {
-                        end = nact;
-                        break;
-                    }
-                    path |= 1ull << q;
-                    mstart |= 1ull << q;
-                    uint32_t len = lane_read(mlen, q);
-                    if (len == kCmpB && n - (ip + q) > kCmpB) {
-                        if (STAMPS)
-                            acc[EC_EXTEND] += 1;
-                        len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
-                        if (STAMPS)
-                            acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
-                        mlen = l == q ? len : mlen;
-                    }
-                    end = q + len;
-                    if (++nmatch >= POM_ENC_PATHMAX) // the window ends after this match
-                        break;
-                }
-            };
-            walk(0);
-
-            ESTAMP(EP_PATH);
-            // ---- exactness: claims among the path lanes, and forwarding ------
-            // Path lane l read h1 (and h2 when use2) and writes slot.  The
-            // table keeps, per hashed slot, the lowest lane of this window
-            // writing it (ds_min of tag|lane; a wave's LDS operations complete
-            // in order, so the reads below see every post).  A path lane is
-            // inexact only if a lower path lane writes a slot it read.  The
-            // first such lane c is decided again: its entry is the position of
-            // the last lower path lane j writing that slot -- less than 64
-            // back, so the candidate passes the M2_MAX_OFFSET test -- and j's
-            // probe words are the candidate's bytes.  The path is walked again
-            // from c and the claims re-posted under a new tag; after
-            // POM_ENC_FWD such rounds the window ends at the next such lane.
-            uint64_t resolved = 0, superseded = 0;   // (superseded: a later lane writes its slot)
-            for (uint32_t round = 0;; round++) {
-                const bool onpath = (path >> l) & 1ull;
-                const uint32_t mine = (wtag << 8) | l;
-                atomicMin(&S.claim[onpath ? claim_index(slot) : kClaim], mine);
-                wave_order();
-                const uint32_t t1 = S.claim[claim_index(h1)];
-                const uint32_t t2 = S.claim[claim_index(h2)];
-                const bool cf1 = ((t1 >> 8) == wtag) & ((t1 & 0xFFu) < l);
-                const bool cf2 = use2 & ((t2 >> 8) == wtag) & ((t2 & 0xFFu) < l);
-                const bool fresh = ((resolved >> l) & 1ull) == 0;
-                const uint64_t cm = wave_ballot(onpath & fresh & (cf1 | cf2));
-                wtag--;
-                if (!cm)
-                    break;
-                const uint32_t c = (uint32_t)__builtin_ctzll(cm);   // never lane 0
-                if (round >= POM_ENC_FWD) {
-                    end = c;                         // the window ends at a path lane
-                    break;
-                }
-                if (STAMPS)
-                    acc[EC_FWD] += 1;
-                resolved |= 1ull << c;
-                const uint64_t below_c = (1ull << c) - 1;
-                const uint64_t pm = path & below_c;  // exact path lanes below c
-                const uint32_t h1c = lane_read(h1, c), h2c = lane_read(h2, c);
-                const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
-                const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (((wave_ballot(use2) >> c) & 1ull) ? ~0ull : 0ull);
-                if (!wm1 && !wm2)
-                    continue;                        // a claim-table alias: c was exact
-                const bool via2 = wm1 == 0;          // h1 unchanged, its test failed again: h2
-                const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
-                superseded |= 1ull << j;             // c writes j's slot after j
-                uint32_t pj[kCmpW];
-#pragma unroll
-                for (int i = 0; i < kCmpW; i++)
-                    pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)pw[i]);
-                uint32_t mc = first_diff<kCmpW>(pj, pw);
-                mc = mc < n - p ? mc : n - p;
-                const bool isc = l == c;
-                ok = isc ? ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0 : ok;
-                mlen = isc ? mc : mlen;
-                cand = isc ? ip + j : cand;
-                slot = isc ? (via2 ? h2 : h1) : slot;
-                use2 = isc ? via2 : use2;
-                okm = wave_ballot(ok);
-                path &= below_c;
-                mstart &= below_c;
-                nmatch = (uint32_t)__builtin_popcountll(mstart);
-                walk(c);
-            }
-            if (STAMPS) {                            // (why the window ended)
-                acc[EC_C2NEED] += end > 64 ? 1 : 0;  // a match crossing its last lane
-                acc[EC_C2MATCH] += nmatch >= POM_ENC_PATHMAX ? 1 : 0;   // the path cap
-            }
-            const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
-
-            uint32_t npw[kCmpW];
-            load_at<kCmpW>(B, ip + end + l, npw);
-
-            ESTAMP(EP_CLAIM);
-            // ---- tokens for the matches before the cut ------------------------
-            // Each match lane writes its own token: its literal run starts
-            // after the highest lane below it that is not a literal path lane
-            // (the last byte of the previous match), or at ii.  The parse
-            // stops after the first match reaching ip_end (:3151-3152).
-            uint64_t km = mstart & keep;
-            const bool ism = (km >> l) & 1ull;
-            const uint64_t dm = wave_ballot(ism && p + mlen >= ip_end);
-            const bool done = dm != 0;
-            if (done) {
-                const uint32_t d = (uint32_t)__builtin_ctzll(dm);
-                km &= d >= 63 ? ~0ull : ((2ull << d) - 1);
-            }
-            if (km) {
-                const uint32_t cnt = (uint32_t)__builtin_popcountll(km);
-                if (STAMPS)
-                    acc[EC_TOKENS] += cnt;
-                ESTAMP(EP_TOK);
-                while (tp + cnt - cons_seen > kTok) {    // the emit wave always drains
-                    __builtin_amdgcn_s_sleep(2);
-                    cons_seen = lds_load(&S.cons);
-                }
-                ESTAMP(EP_PUSHWAIT);
-                const uint64_t below = (1ull << l) - 1;
-                const uint64_t stop = ~(path & ~mstart) & below;
-                const uint32_t from = stop ? ip + 64 - (uint32_t)__builtin_clzll(stop) : ii;
-                const uint32_t r = (uint32_t)__builtin_popcountll(km & below);
-                S.tok[(km >> l) & 1ull ? (tp + r) % kTok : kTok] = make_uint4(from, p - from, mlen, p - cand);
-                tp += cnt;
-                lds_store(&S.prod, tp);
-                const uint32_t last = 63 - (uint32_t)__builtin_clzll(km);
-                ii = ip + last + lane_read(mlen, last);
-            }
-            // UPDATE_I of every path lane before the cut but the superseded ones: their slots are distinct
-            ESTAMP(EP_TOK);
-            if (GD) {
-                if ((path & keep & ~superseded) >> l & 1ull)
-                    D.put(slot, p - base + 1);
-            } else {
-                D.put((path & keep & ~superseded) >> l & 1ull ? slot : kSlots, p - base + 1);
-            }
-            wave_order();
-            ESTAMP(EP_DICT);
-            if (done)
-                break;
-            ip += end;
-            if (ip >= ip_end)
-                break;
-#pragma unroll
-            for (int i = 0; i < kCmpW; i++)
-                pw[i] = npw[i];
-        }
-    }
-    push(ii, n - ii, 0, 0);                          // tail + EOF
-#undef ESTAMP
-}
-
-// ---------------------------------------------------------------------------
 // Emitter: tokens -> the LZO1X byte stream (lzo1x_emit.h) in an LDS ring,
 // stored to HBM.  Run by the emit wave (two-wave kernels) or, in the fused
 // kernel, by the parse wave itself after each window.
@@ -556,10 +267,14 @@ struct Emitter {
     uint32_t ct;                                     // tokens consumed
     uint32_t pos;                                    // input covered by the tokens so far
     bool poisoned;                                   // a token the parse cannot have meant
+    uint32_t* olen;                                  // out_len / status / block of drain(prod)
+    int32_t* ost;
+    uint32_t blk;
 
     __device__ __forceinline__ Emitter(EncLdsT<GD>& S_, const uint8_t* in, uint32_t n_, uint8_t* out,
                                        uint32_t cap)
-        : S(S_), B(block_src(in, n_)), n(n_), ct(0), pos(0), poisoned(false)
+        : S(S_), B(block_src(in, n_)), n(n_), ct(0), pos(0), poisoned(false), olen(nullptr),
+          ost(nullptr), blk(0)
     {
         e.in = in;
         e.n = n_;
@@ -724,7 +439,350 @@ struct Emitter {
         }
         return false;
     }
+    __device__ bool drain(uint32_t prod) { return drain(prod, olen, ost, blk); }
 };
+
+// ---------------------------------------------------------------------------
+// Parse wave
+// ---------------------------------------------------------------------------
+// Diagnostic build only (STAMPS): per-phase s_memtime cycle sums and counts of
+// the parse wave go to stamps[b * kEncStampSlots + i]; no output depends on them.
+enum { EP_SETUP, EP_PROBE, EP_CAND, EP_PATH, EP_CLAIM, EP_TOK, EP_DICT, EP_PUSHWAIT,
+       EC_WINDOWS, EC_EXTEND, EC_TOKENS, EC_PATHIT, EC_EXTIT, EC_C2NEED, EC_C2MATCH, EC_FWD, EP_N };
+constexpr int kEncStampSlots = 16;
+
+// FUSED (one-wave kernel): the parse wave runs the emitter E itself -- it
+// drains the token queue once POM_ENC_DRAIN tokens are pending (larger emit
+// batches than an eager emit wave gets) or the queue has no room, and at the
+// end -- and pulls the lines ahead of the parse into L2 as the emit wave does.
+#ifndef POM_ENC_DRAIN
+#define POM_ENC_DRAIN 32
+#endif
+template <bool STAMPS, bool GD, bool FUSED = false>
+__device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, uint32_t n, uint32_t l,
+                           uint64_t* acc, Emitter<GD>* E = nullptr)
+{
+    uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+#define ESTAMP(ph)                                                  \
+    do {                                                            \
+        if (STAMPS) {                                               \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+            acc[ph] += now_ - tmark;                                \
+            tmark = now_;                                           \
+        }                                                           \
+    } while (0)
+    uint32_t tp = 0;                                // tokens produced
+    uint32_t cons_seen = 0;
+    // (FUSED) lines up to POM_ENC_AHEAD bytes past the window go to L2, one
+    // dword per 128-B line; the loaded words are folded in a window later, so
+    // the parse never waits on them.
+    const uintptr_t pf_lines = (uintptr_t)in & ~(uintptr_t)127;
+    const uintptr_t pf_last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
+    uint32_t pf = 0, pf_acc = 0, pf_new = 0;
+    auto prefetch = [&](uint32_t at) {
+        pf_acc ^= pf_new;
+        pf_new = 0;
+        const uint32_t ahead = at + POM_ENC_AHEAD;
+        const uint32_t want = ahead < n + 127 ? ahead : n + 127;
+        for (; pf < want; pf += 128 * kWave) {
+            const uintptr_t a = pf_lines + pf + 128 * l;
+            if (a <= pf_last)
+                pf_new ^= *(gdword*)a;
+        }
+    };
+    auto push = [&](uint32_t from, uint32_t nlit, uint32_t mlen, uint32_t off) {
+        if (STAMPS)
+            acc[EC_TOKENS] += 1;
+        ESTAMP(EP_TOK);
+        if (FUSED) {
+            if (tp - E->ct >= kTok)
+                E->drain(tp);
+        } else {
+            while (tp - cons_seen >= kTok) {         // the emit wave always drains
+                __builtin_amdgcn_s_sleep(2);
+                cons_seen = lds_load(&S.cons);
+            }
+        }
+        ESTAMP(EP_PUSHWAIT);
+        if (l == 0)
+            S.tok[tp % kTok] = make_uint4(from, nlit, mlen, off);
+        tp++;
+        lds_store(&S.prod, tp);
+    };
+
+    const BlockSrc B = block_src(in, n);
+    uint32_t ii = 0;                                // first byte not yet emitted
+    if (n > 13) {                                   // lib/minilzo.c:3167-3173
+        for (uint32_t s = l; s < kSlots / 2; s += kWave)
+            D.put2(s, 0);                           // zero-filled wrkmem: all EMPTY
+        for (uint32_t s = l; s < kClaim; s += kWave)
+            S.claim[s] = 0xFFFFFFFFu;               // (tag 0xFFFFFF: no window has it)
+        if (GD)
+            __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0): the table is zero in L2
+        wave_order();
+        const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
+        uint32_t ip = 4;
+        uint32_t base = 0;                          // dictionary position base
+        uint32_t wtag = 0xFFFFFEu;                  // claim tag of the window (one per window, > 0)
+        // Probe words of the window (position ip + l): the next window's are
+        // read as soon as its start is known, ahead of the token and
+        // dictionary writes.
+        uint32_t pw[kCmpW];
+        load_at<kCmpW>(B, ip + l, pw);
+        ESTAMP(EP_SETUP);
+        for (;;) {
+            if (STAMPS)
+                acc[EC_WINDOWS] += 1;
+            if (ip + kWave - base >= 0xFFFFu) {     // this window's positions would not fit
+                const uint32_t nb = (ip - (kM4MaxOffset + 1)) / kRebase * kRebase;
+                const uint32_t delta = nb - base;
+                for (uint32_t s2 = l; s2 < kSlots / 2; s2 += kWave) {
+                    const uint32_t pr = D.get2(s2);
+                    const uint32_t lo = pr & 0xFFFFu, hi = pr >> 16;
+                    const uint32_t nlo = lo > delta ? lo - delta : 0u;
+                    const uint32_t nhi = hi > delta ? hi - delta : 0u;
+                    D.put2(s2, nlo | (nhi << 16));
+                }
+                if (GD)
+                    __builtin_amdgcn_s_waitcnt(0x0F70);
+                wave_order();
+                base = nb;
+            }
+            if (POM_ENC_AHEAD) {
+                if (FUSED)
+                    prefetch(ip);
+                else
+                    S.ip = ip;
+            }
+            const uint32_t p = ip + l;
+            const bool active = l == 0 || p < ip_end;   // the first probe always runs
+            // (every lane probes; an inactive one ends with no candidate)
+            const uint32_t h1 = emit::slot_primary(pw[0] & 0xFF, (pw[0] >> 8) & 0xFF,
+                                                   (pw[0] >> 16) & 0xFF, pw[0] >> 24);
+            const uint32_t h2 = emit::slot_secondary(h1);
+            const uint32_t e1 = D.get(h1), e2 = D.get(h2);
+            const uint32_t w1 = active && e1 ? base + e1 - 1 : 0u;   // (positions >= 4: 0 stays "empty")
+            const uint32_t w2 = active && e2 ? base + e2 - 1 : 0u;
+            const uint64_t am = mask_lt(p, ip_end) | 1ull;      // (active)
+            const uint32_t nact = (uint32_t)__builtin_popcountll(am);
+            if (STAMPS)
+                __builtin_amdgcn_s_waitcnt(0);       // (attribute the probe loads here)
+            ESTAMP(EP_PROBE);
+
+            // Probe decision of every active lane with the pre-window
+            // dictionary, lib/minilzo.c:2940-2971 (exact up to the cut below).
+            const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
+            const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
+            uint32_t c1w[kCmpW], c2w[kCmpW];        // (read unconditionally; used only if valid)
+            load_at<kCmpW>(B, w1, c1w);
+            load_at<kCmpW>(B, w2, c2w);
+            const uint32_t b3 = pw[0] >> 24;
+            // (selects, no branches)
+            const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
+            bool use2 = v1 && !c1pass;               // the secondary slot is read and written
+            const bool c2pass = use2 && v2 && (p - w2 <= kM2MaxOffset || (c2w[0] >> 24) == b3);
+            const bool tm = c1pass || c2pass;
+            uint32_t slot = use2 ? h2 : h1, cand = c2pass ? w2 : w1;
+            uint32_t cw[kCmpW];
+#pragma unroll
+            for (int i = 0; i < kCmpW; i++)
+                cw[i] = c2pass ? c2w[i] : c1w[i];
+            // try_match (:2962-2971), then the match length as far as kCmpB bytes
+            bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
+            uint32_t mlen = first_diff<kCmpW>(cw, pw);
+            mlen = mlen < n - p ? mlen : n - p;
+
+            // ---- the greedy path through the window, speculatively ----------
+            // From lane 0: a matching lane jumps over its match, any other
+            // lane is a literal.  Lanes inside matches neither probe nor
+            // update the dictionary (:3051-3150).
+            uint64_t okm = wave_ballot(ok);
+            if (STAMPS) {
+                __builtin_amdgcn_s_waitcnt(0);       // (attribute the candidate loads here)
+                acc[EC_C2NEED] += 0;
+                acc[EC_C2MATCH] += 0;
+            }
+            ESTAMP(EP_CAND);
+            uint64_t path = 0, mstart = 0;
+            uint32_t end = 0;                        // lane where the path leaves the window
+            uint32_t nmatch = 0;
+            // the path from lane `from` on (lanes below it stay as they are)
+            auto walk = [&](uint32_t from) {
+                end = from;
+                while (end < nact) {
+                    if (STAMPS)
+                        acc[EC_PATHIT] += 1;
+                    const uint64_t rest = okm & (~0ull << end);
+                    const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
+                    const uint32_t lit_end = q < nact ? q : nact;
+                    if (lit_end > end)               // literal lanes end .. lit_end-1
+                        path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
+                    if (q >= nact) {
+                        end = nact;
+                        break;
+                    }
+                    path |= 1ull << q;
+                    mstart |= 1ull << q;
+                    uint32_t len = lane_read(mlen, q);
+                    if (len == kCmpB && n - (ip + q) > kCmpB) {
+                        if (STAMPS)
+                            acc[EC_EXTEND] += 1;
+                        len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
+                        if (STAMPS)
+                            acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
+                        mlen = l == q ? len : mlen;
+                    }
+                    end = q + len;
+                    if (++nmatch >= POM_ENC_PATHMAX) // the window ends after this match
+                        break;
+                }
+            };
+            walk(0);
+
+            ESTAMP(EP_PATH);
+            // ---- exactness: claims among the path lanes, and forwarding ------
+            // Path lane l read h1 (and h2 when use2) and writes slot.  The
+            // table keeps, per hashed slot, the lowest lane of this window
+            // writing it (ds_min of tag|lane; a wave's LDS operations complete
+            // in order, so the reads below see every post).  A path lane is
+            // inexact only if a lower path lane writes a slot it read.  The
+            // first such lane c is decided again: its entry is the position of
+            // the last lower path lane j writing that slot -- less than 64
+            // back, so the candidate passes the M2_MAX_OFFSET test -- and j's
+            // probe words are the candidate's bytes.  The path is walked again
+            // from c and the claims re-posted under a new tag; after
+            // POM_ENC_FWD such rounds the window ends at the next such lane.
+            uint64_t resolved = 0, superseded = 0;   // (superseded: a later lane writes its slot)
+            uint64_t um2 = wave_ballot(use2);        // lanes that read the secondary slot
+            for (uint32_t round = 0;; round++) {
+                const bool onpath = (path >> l) & 1ull;
+                const uint32_t mine = (wtag << 8) | l;
+                atomicMin(&S.claim[onpath ? claim_index(slot) : kClaim], mine);
+                wave_order();
+                const uint32_t t1 = S.claim[claim_index(h1)];
+                const uint32_t t2 = S.claim[claim_index(h2)];
+                // path lanes not yet resolved that read a slot a lower lane of
+                // this window writes (h1, or h2 when use2)
+                const uint64_t cf1 = mask_eq(t1 >> 8, wtag) & mask_lt(t1 & 0xFFu, l);
+                const uint64_t cf2 = um2 & mask_eq(t2 >> 8, wtag) & mask_lt(t2 & 0xFFu, l);
+                const uint64_t cm = path & ~resolved & (cf1 | cf2);
+                wtag--;
+                if (!cm)
+                    break;
+                const uint32_t c = (uint32_t)__builtin_ctzll(cm);   // never lane 0
+                if (round >= POM_ENC_FWD) {
+                    end = c;                         // the window ends at a path lane
+                    break;
+                }
+                if (STAMPS)
+                    acc[EC_FWD] += 1;
+                resolved |= 1ull << c;
+                const uint64_t below_c = (1ull << c) - 1;
+                const uint64_t pm = path & below_c;  // exact path lanes below c
+                const uint32_t h1c = lane_read(h1, c), h2c = lane_read(h2, c);
+                const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
+                const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (((um2 >> c) & 1ull) ? ~0ull : 0ull);
+                if (!wm1 && !wm2)
+                    continue;                        // a claim-table alias: c was exact
+                const bool via2 = wm1 == 0;          // h1 unchanged, its test failed again: h2
+                const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
+                superseded |= 1ull << j;             // c writes j's slot after j
+                uint32_t pj[kCmpW];
+#pragma unroll
+                for (int i = 0; i < kCmpW; i++)
+                    pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)pw[i]);
+                uint32_t mc = first_diff<kCmpW>(pj, pw);
+                mc = mc < n - p ? mc : n - p;
+                const bool isc = l == c;
+                ok = isc ? ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0 : ok;
+                mlen = isc ? mc : mlen;
+                cand = isc ? ip + j : cand;
+                slot = isc ? (via2 ? h2 : h1) : slot;
+                use2 = isc ? via2 : use2;
+                um2 = via2 ? um2 | (1ull << c) : um2 & ~(1ull << c);
+                okm = wave_ballot(ok);
+                path &= below_c;
+                mstart &= below_c;
+                nmatch = (uint32_t)__builtin_popcountll(mstart);
+                walk(c);
+            }
+            if (STAMPS) {                            // (why the window ended)
+                acc[EC_C2NEED] += end > 64 ? 1 : 0;  // a match crossing its last lane
+                acc[EC_C2MATCH] += nmatch >= POM_ENC_PATHMAX ? 1 : 0;   // the path cap
+            }
+            const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
+
+            uint32_t npw[kCmpW];
+            load_at<kCmpW>(B, ip + end + l, npw);
+
+            ESTAMP(EP_CLAIM);
+            // ---- tokens for the matches before the cut ------------------------
+            // Each match lane writes its own token: its literal run starts
+            // after the highest lane below it that is not a literal path lane
+            // (the last byte of the previous match), or at ii.  The parse
+            // stops after the first match reaching ip_end (:3151-3152).
+            uint64_t km = mstart & keep;
+            const uint64_t dm = km & mask_ge(p + mlen, ip_end);   // (ism && p + mlen >= ip_end)
+            const bool done = dm != 0;
+            if (done) {
+                const uint32_t d = (uint32_t)__builtin_ctzll(dm);
+                km &= d >= 63 ? ~0ull : ((2ull << d) - 1);
+            }
+            if (km) {
+                const uint32_t cnt = (uint32_t)__builtin_popcountll(km);
+                if (STAMPS)
+                    acc[EC_TOKENS] += cnt;
+                ESTAMP(EP_TOK);
+                if (FUSED) {
+                    if (tp + cnt - E->ct > kTok)
+                        E->drain(tp);
+                } else {
+                    while (tp + cnt - cons_seen > kTok) {    // the emit wave always drains
+                        __builtin_amdgcn_s_sleep(2);
+                        cons_seen = lds_load(&S.cons);
+                    }
+                }
+                ESTAMP(EP_PUSHWAIT);
+                const uint64_t below = (1ull << l) - 1;
+                const uint64_t stop = ~(path & ~mstart) & below;
+                const uint32_t from = stop ? ip + 64 - (uint32_t)__builtin_clzll(stop) : ii;
+                const uint32_t r = (uint32_t)__builtin_popcountll(km & below);
+                S.tok[(km >> l) & 1ull ? (tp + r) % kTok : kTok] = make_uint4(from, p - from, mlen, p - cand);
+                tp += cnt;
+                lds_store(&S.prod, tp);
+                const uint32_t last = 63 - (uint32_t)__builtin_clzll(km);
+                ii = ip + last + lane_read(mlen, last);
+                if (FUSED && tp - E->ct >= POM_ENC_DRAIN)
+                    E->drain(tp);
+            }
+            // UPDATE_I of every path lane before the cut but the superseded ones: their slots are distinct
+            ESTAMP(EP_TOK);
+            if (GD) {
+                if ((path & keep & ~superseded) >> l & 1ull)
+                    D.put(slot, p - base + 1);
+            } else {
+                D.put((path & keep & ~superseded) >> l & 1ull ? slot : kSlots, p - base + 1);
+            }
+            wave_order();
+            ESTAMP(EP_DICT);
+            if (done)
+                break;
+            ip += end;
+            if (ip >= ip_end)
+                break;
+#pragma unroll
+            for (int i = 0; i < kCmpW; i++)
+                pw[i] = npw[i];
+        }
+    }
+    push(ii, n - ii, 0, 0);                          // tail + EOF
+    if (FUSED) {
+        E->drain(tp);                                // through the tail: out_len, status set
+        if (pf_acc == 0x9E3779B9u)                   // (keeps the prefetch loads; never matters)
+            S.sink = pf_acc;
+    }
+#undef ESTAMP
+}
 
 // Emit wave (two-wave kernels): drains the token queue as the parse wave
 // fills it.
@@ -846,7 +904,59 @@ __global__ __launch_bounds__(2 * kWave, POM_ENC_RESIDENT / 2) void lzo1x_encode_
     }
 }
 
+// One-wave global-dictionary encoder: the parse wave emits its own tokens
+// (parse_wave<..., FUSED>), so a CU holds POM_ENC_RESIDENT1 blocks in flight
+// instead of 16 -- more independent parse chains per SIMD to hide the probe
+// and candidate round trips.
+#ifndef POM_ENC_RESIDENT1
+#define POM_ENC_RESIDENT1 24                    // one-wave workgroups per CU (6 waves per SIMD)
+#endif
+static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT1 <= 160 * 1024, "LDS budget");
+
+__global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdict1_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
+    uint8_t* __restrict__ dicts)
+{
+    __shared__ EncLdsT<true> S;
+    Dict<true> D;
+    D.lds = nullptr;
+    D.g = (gu16*)(dicts + (size_t)blockIdx.x * kDictBytes);
+    const uint32_t l = lane_id();
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint32_t n = src_len[b];
+        if (n > kMaxN) {                             // the general encoder's
+            if (l == 0)
+                status[b] = LZO_MI355X_ENC_PENDING;
+            continue;
+        }
+        const uint8_t* in = src + src_off[b];
+        Emitter<true> E(S, in, n, dst + dst_off[b], dst_cap[b]);
+        E.olen = out_len;
+        E.ost = status;
+        E.blk = b;
+        uint64_t acc[EP_N];
+        parse_wave<false, true, true>(S, D, in, n, l, acc, &E);
+        wave_order();
+    }
+}
+
 }  // namespace
+
+// Waves per block of the global-dictionary encoder: POM_ENC_WAVES (1 or 2,
+// read at every launch, for A/B runs and the tests of both kernels), default
+// POM_ENC_WAVES_DEFAULT.
+#ifndef POM_ENC_WAVES_DEFAULT
+#define POM_ENC_WAVES_DEFAULT 2
+#endif
+static int enc_waves(void)
+{
+    const char* e = getenv("POM_ENC_WAVES");
+    const int w = e ? atoi(e) : POM_ENC_WAVES_DEFAULT;
+    return w == 1 ? 1 : 2;
+}
 
 static uint32_t enc_resident(void)
 {
@@ -860,7 +970,7 @@ static uint32_t enc_resident(void)
             n = 256;
         cus[dev] = n;
     }
-    return (uint32_t)cus[dev] * POM_ENC_RESIDENT;
+    return (uint32_t)cus[dev] * (enc_waves() == 1 ? POM_ENC_RESIDENT1 : POM_ENC_RESIDENT);
 }
 
 extern "C" size_t lzo_mi355x_compress_scratch(uint32_t nblocks)
@@ -881,7 +991,10 @@ extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_
     uint32_t grid = scratch ? (uint32_t)(scratch_bytes / kDictBytes) : 0u;
     grid = grid < nblocks ? grid : nblocks;
     grid = grid < enc_resident() ? grid : enc_resident();
-    if (grid)
+    if (grid && enc_waves() == 1)
+        hipLaunchKernelGGL(lzo1x_encode_gdict1_kernel, dim3(grid), dim3(kWave), 0, stream, src, src_off,
+                           src_len, dst, dst_off, dst_cap, out_len, status, nblocks, (uint8_t*)scratch);
+    else if (grid)
         hipLaunchKernelGGL(lzo1x_encode_gdict_kernel<false>, dim3(grid), dim3(2 * kWave), 0, stream,
                            src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
                            (uint8_t*)scratch, nullptr);

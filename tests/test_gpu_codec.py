@@ -540,3 +540,30 @@ def test_host_batch_api_many_mixed_blocks(dev, oracle):
     rc, st, outs = lzo.decompress_batch(comps, [len(b) for b in blocks])
     assert rc == 0 and all(s == 0 for s in st)
     assert outs == blocks
+
+
+@pytest.mark.parametrize("kernel", ["gdict_one_wave", "gdict_two_wave", "lds"])
+def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
+    """Each throughput encoder kernel (global dictionary with one or two waves
+    per block, LDS dictionary) byte-identical to the oracle on the sweep's
+    content models, sizes up to 300 KB, more blocks than one grid holds."""
+    if kernel == "gdict_two_wave":
+        monkeypatch.setenv("POM_ENC_WAVES", "2")
+    elif kernel == "gdict_one_wave":
+        monkeypatch.setenv("POM_ENC_WAVES", "1")
+    blocks = _sweep_blocks(300, 91)
+    src = gu.device_batch(torch, blocks, dev, shift=1)
+    dst = gu.empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
+    olen = torch.zeros(len(blocks), dtype=torch.int32, device=dev)
+    st = torch.full((len(blocks),), 99, dtype=torch.int32, device=dev)
+    if kernel == "lds":
+        lzo.compress_dev(src, dst, olen, st, scratch=None)
+    else:
+        # a grid of 40 workgroups: each dictionary region serves several blocks
+        scr = torch.empty(lzo.compress_scratch_bytes(40), dtype=torch.uint8, device=dev)
+        lzo.compress_dev(src, dst, olen, st, scratch=scr)
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(blocks)
+    comps = gu.fetch(dst, olen)
+    bad = [i for i, (b, c) in enumerate(zip(blocks, comps)) if c != oracle.compress(b)]
+    assert not bad, bad[:10]
