@@ -909,7 +909,7 @@ __global__ __launch_bounds__(2 * kWave, POM_ENC_RESIDENT / 2) void lzo1x_encode_
 // instead of 16 -- more independent parse chains per SIMD to hide the probe
 // and candidate round trips.
 #ifndef POM_ENC_RESIDENT1
-#define POM_ENC_RESIDENT1 24                    // one-wave workgroups per CU (6 waves per SIMD)
+#define POM_ENC_RESIDENT1 16                    // one-wave workgroups per CU (4 waves per SIMD: 128 VGPRs, no spills)
 #endif
 static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT1 <= 160 * 1024, "LDS budget");
 
@@ -949,7 +949,7 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
 // read at every launch, for A/B runs and the tests of both kernels), default
 // POM_ENC_WAVES_DEFAULT.
 #ifndef POM_ENC_WAVES_DEFAULT
-#define POM_ENC_WAVES_DEFAULT 2
+#define POM_ENC_WAVES_DEFAULT 1
 #endif
 static int enc_waves(void)
 {
