@@ -213,6 +213,9 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 #ifndef POM_ENC_BATCH
 #define POM_ENC_BATCH 1                          // the emit wave writes up to 64 tokens per pass
 #endif
+#ifndef POM_ENC_FARINV
+#define POM_ENC_FARINV 1
+#endif
 #ifndef POM_ENC_FWD
 #define POM_ENC_FWD 8                            // claim conflicts resolved in place per window
 #endif
@@ -574,8 +577,15 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
             const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
             uint32_t c1w[kCmpW], c2w[kCmpW];        // (read unconditionally; used only if valid)
+#if POM_ENC_FARINV
+            // (lanes without a valid candidate read past the block: range
+            // checked, no memory request)
+            load_at<kCmpW>(B, v1 ? w1 : kFarPos, c1w);
+            load_at<kCmpW>(B, v2 ? w2 : kFarPos, c2w);
+#else
             load_at<kCmpW>(B, w1, c1w);
             load_at<kCmpW>(B, w2, c2w);
+#endif
             const uint32_t b3 = pw[0] >> 24;
             // (selects, no branches)
             const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
