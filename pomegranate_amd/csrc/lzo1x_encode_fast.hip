@@ -579,9 +579,11 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             uint32_t c1w[kCmpW], c2w[kCmpW];        // (read unconditionally; used only if valid)
 #if POM_ENC_FARINV
             // (lanes without a valid candidate read past the block: range
-            // checked, no memory request)
+            // checked, no memory request; the secondary candidate is only
+            // ever compared when the primary one is more than M2_MAX_OFFSET
+            // back, lib/minilzo.c:2946-2949)
             load_at<kCmpW>(B, v1 ? w1 : kFarPos, c1w);
-            load_at<kCmpW>(B, v2 ? w2 : kFarPos, c2w);
+            load_at<kCmpW>(B, v2 && p - w1 > kM2MaxOffset ? w2 : kFarPos, c2w);
 #else
             load_at<kCmpW>(B, w1, c1w);
             load_at<kCmpW>(B, w2, c2w);
