@@ -45,7 +45,7 @@ def solo_avg_ns(kname):
             if r["Stream_Id"] == rows[0]["Stream_Id"]]
     return statistics.mean(solo), len(solo)
 KERNEL = {"decode": ("decode_fast_kernel", "lzo1x_decode_fast_kernel"),
-          "encode": ("encode_gdict_kernel", "lzo1x_encode_gdict_kernel")}
+          "encode": ("encode_gdict1_kernel", "lzo1x_encode_gdict1_kernel")}   # (one-wave default)
 
 
 def counters(op, name):
