@@ -37,7 +37,9 @@ int lzo_mi355x_device_count(void);
  */
 /* `scratch`: device memory of lzo_mi355x_compress_scratch(nblocks) bytes for
  * the per-workgroup match dictionaries (32 KiB each; 16 blocks per CU are then
- * parsed at once), or NULL (dictionaries in LDS: 4 blocks per CU). */
+ * parsed at once) after a 256-byte head (the block ticket of batches larger
+ * than the grid, reset by the call on `stream`), or NULL (dictionaries in LDS:
+ * 4 blocks per CU).  No initial contents are required. */
 int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                             const uint32_t *src_len, uint8_t *dst,
                             const uint64_t *dst_off, const uint32_t *dst_cap,

@@ -77,6 +77,10 @@ constexpr uint32_t kFarPos = 0xC0000000u;        // a read position past every b
 #endif
 constexpr uint32_t kDictBytes = (kSlots + 2) * 2 + 60;   // per workgroup, 64-byte multiple
 static_assert(kDictBytes % 64 == 0, "dictionary regions stay 64-byte aligned");
+// Scratch: [0, kScratchHead) the block ticket counter (u32, zeroed by the
+// launcher when the grid is smaller than the batch), then one dictionary
+// region per workgroup.
+constexpr uint32_t kScratchHead = 256;
 
 template <bool GD>
 struct __attribute__((aligned(16))) EncLdsT {
@@ -895,8 +899,19 @@ __global__ __launch_bounds__(2 * kWave) void lzo1x_encode_fast_kernel(
                                 b, stamps);
 }
 
-// Global-dictionary encoder: a grid of resident workgroups, each with its
-// own dictionary region, working through the blocks grid-stride.
+// Global-dictionary encoders: a grid of resident workgroups, each with its
+// own dictionary region.  Workgroup g codes block g, then (when the batch has
+// more blocks than the grid) takes block gridDim.x + ticket++ until none is
+// left: a workgroup that drew small blocks takes more of them, so mixed sizes
+// (C4: 4-256 KiB) finish together instead of with the unluckiest stride.
+__device__ __forceinline__ uint32_t next_block(uint32_t* ticket)
+{
+    uint32_t t = 0;
+    if (lane_id() == 0)
+        t = atomicAdd(ticket, 1u);
+    return gridDim.x + __builtin_amdgcn_readfirstlane(t);
+}
+
 template <bool STAMPS>
 __global__ __launch_bounds__(2 * kWave, POM_ENC_RESIDENT / 2) void lzo1x_encode_gdict_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
@@ -906,13 +921,24 @@ __global__ __launch_bounds__(2 * kWave, POM_ENC_RESIDENT / 2) void lzo1x_encode_
     uint8_t* __restrict__ dicts, uint64_t* __restrict__ stamps)
 {
     __shared__ EncLdsT<true> S;
+    __shared__ uint32_t next;
     Dict<true> D;
     D.lds = nullptr;
-    D.g = (gu16*)(dicts + (size_t)blockIdx.x * kDictBytes);
-    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    D.g = (gu16*)(dicts + kScratchHead + (size_t)blockIdx.x * kDictBytes);
+    const bool dyn = nblocks > gridDim.x;
+    for (uint32_t b = blockIdx.x; b < nblocks;) {
         encode_block<STAMPS, true>(S, D, src, src_off, src_len, dst, dst_off, dst_cap, out_len,
                                    status, b, stamps);
-        __syncthreads();                             // both waves done with the block
+        if (!dyn)
+            break;
+        if (threadIdx.x < kWave) {
+            const uint32_t nb = next_block((uint32_t*)dicts);
+            if (threadIdx.x == 0)
+                next = nb;
+        }
+        __syncthreads();                             // both waves done with the block; `next` set
+        b = next;
+        __syncthreads();                             // (read before the next block overwrites it)
     }
 }
 
@@ -935,9 +961,10 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
     __shared__ EncLdsT<true> S;
     Dict<true> D;
     D.lds = nullptr;
-    D.g = (gu16*)(dicts + (size_t)blockIdx.x * kDictBytes);
+    D.g = (gu16*)(dicts + kScratchHead + (size_t)blockIdx.x * kDictBytes);
     const uint32_t l = lane_id();
-    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    const bool dyn = nblocks > gridDim.x;
+    for (uint32_t b = blockIdx.x; b < nblocks; b = dyn ? next_block((uint32_t*)dicts) : nblocks) {
         const uint32_t n = src_len[b];
         if (n > kMaxN) {                             // the general encoder's
             if (l == 0)
@@ -985,10 +1012,23 @@ static uint32_t enc_resident(void)
     return (uint32_t)cus[dev] * (enc_waves() == 1 ? POM_ENC_RESIDENT1 : POM_ENC_RESIDENT);
 }
 
+// Grid of the global-dictionary encoders: one workgroup per dictionary region
+// of the scratch, at most one per block and one per resident slot, and at
+// most POM_ENC_GRID (tests: a grid smaller than the batch).
+static uint32_t enc_grid(size_t scratch_bytes, uint32_t nblocks)
+{
+    uint32_t grid = scratch_bytes > kScratchHead ? (uint32_t)((scratch_bytes - kScratchHead) / kDictBytes) : 0u;
+    grid = grid < nblocks ? grid : nblocks;
+    grid = grid < enc_resident() ? grid : enc_resident();
+    const char* e = getenv("POM_ENC_GRID");
+    const uint32_t cap = e ? (uint32_t)atoi(e) : 0u;
+    return cap && cap < grid ? cap : grid;
+}
+
 extern "C" size_t lzo_mi355x_compress_scratch(uint32_t nblocks)
 {
     const uint32_t g = nblocks < enc_resident() ? nblocks : enc_resident();
-    return (size_t)g * kDictBytes;
+    return kScratchHead + (size_t)g * kDictBytes;
 }
 
 extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_t* src_off,
@@ -1000,9 +1040,9 @@ extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_
 {
     if (nblocks == 0)
         return 0;
-    uint32_t grid = scratch ? (uint32_t)(scratch_bytes / kDictBytes) : 0u;
-    grid = grid < nblocks ? grid : nblocks;
-    grid = grid < enc_resident() ? grid : enc_resident();
+    const uint32_t grid = scratch ? enc_grid(scratch_bytes, nblocks) : 0u;
+    if (grid && grid < nblocks && hipMemsetAsync(scratch, 0, sizeof(uint32_t), stream) != hipSuccess)
+        return -1;                                   // (the block ticket)
     if (grid && enc_waves() == 1)
         hipLaunchKernelGGL(lzo1x_encode_gdict1_kernel, dim3(grid), dim3(kWave), 0, stream, src, src_off,
                            src_len, dst, dst_off, dst_cap, out_len, status, nblocks, (uint8_t*)scratch);
@@ -1042,10 +1082,8 @@ extern "C" int lzo_mi355x_debug_compress_gdict_stamps(const uint8_t* src, const 
                                                       void* scratch, size_t scratch_bytes,
                                                       uint64_t* stamps, hipStream_t stream)
 {
-    uint32_t grid = (uint32_t)(scratch_bytes / kDictBytes);
-    grid = grid < nblocks ? grid : nblocks;
-    grid = grid < enc_resident() ? grid : enc_resident();
-    if (grid == 0)
+    const uint32_t grid = enc_grid(scratch_bytes, nblocks);
+    if (grid == 0 || (grid < nblocks && hipMemsetAsync(scratch, 0, sizeof(uint32_t), stream) != hipSuccess))
         return -1;
     hipLaunchKernelGGL(lzo1x_encode_gdict_kernel<true>, dim3(grid), dim3(2 * kWave), 0, stream,
                        src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,

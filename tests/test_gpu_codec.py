@@ -559,8 +559,11 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
     if kernel == "lds":
         lzo.compress_dev(src, dst, olen, st, scratch=None)
     else:
-        # a grid of 40 workgroups: each dictionary region serves several blocks
-        scr = torch.empty(lzo.compress_scratch_bytes(40), dtype=torch.uint8, device=dev)
+        # a grid of 40 workgroups: each dictionary region serves several blocks,
+        # taken through the block ticket (scratch sized for the batch, as the
+        # ABI requires; its ticket word starts as garbage)
+        monkeypatch.setenv("POM_ENC_GRID", "40")
+        scr = torch.full((lzo.compress_scratch_bytes(len(blocks)),), 0x5A, dtype=torch.uint8, device=dev)
         lzo.compress_dev(src, dst, olen, st, scratch=scr)
     torch.cuda.synchronize()
     assert st.cpu().numpy().tolist() == [0] * len(blocks)
