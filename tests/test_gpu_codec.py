@@ -570,3 +570,43 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
     comps = gu.fetch(dst, olen)
     bad = [i for i, (b, c) in enumerate(zip(blocks, comps)) if c != oracle.compress(b)]
     assert not bad, bad[:10]
+
+
+@pytest.mark.gpu
+def test_encoder_block_tickets_mixed_sizes(dev, gu):
+    """More blocks than the global-dictionary grid, of mixed ITB sizes (C4's
+    4-256 KiB): workgroups past their first block draw the next one from the
+    ticket counter in the scratch head, whose word starts as garbage.  Every
+    block byte-identical to the LDS-dictionary kernel (itself pinned to the
+    oracle above), then decoded back."""
+    n = 6000                                     # > 4096 resident on a 256-CU MI355X
+    sizes = synth.mixed_sizes(n, 77)
+    arena, offs, lens = synth.batch(synth.ITB, 0, sizes, align=256, threads=16)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    src = lzo.DeviceBatch(t(arena), t(offs.view(np.int64)), t(lens.view(np.int32)))
+    caps = [lzo.worst_compress(int(s)) for s in sizes]
+    outs = []
+    for scratch in ("tickets", None):
+        dst = gu.empty_batch(torch, caps, dev, fill=0xA5)
+        olen = torch.zeros(n, dtype=torch.int32, device=dev)
+        st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+        scr = None
+        if scratch:
+            scr = torch.full((lzo.compress_scratch_bytes(n),), 0xFF, dtype=torch.uint8, device=dev)
+        lzo.compress_dev(src, dst, olen, st, scratch=scr)
+        torch.cuda.synchronize()
+        assert int((st != 0).sum().item()) == 0
+        outs.append((dst, olen))
+    (d1, l1), (d2, l2) = outs
+    assert torch.equal(l1, l2)
+    assert torch.equal(d1.arena, d2.arena)      # (same layout, same 0xA5 fill past each block)
+    zsrc = lzo.DeviceBatch(d1.arena, d1.off, l1)
+    back = torch.zeros_like(src.arena)
+    ob = lzo.DeviceBatch(back, src.off, src.length)
+    ol = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.zeros_like(ol)
+    scr = torch.zeros(lzo.decompress_scratch_bytes(n), dtype=torch.uint8, device=dev)
+    lzo.decompress_dev(zsrc, ob, ol, st, scr)
+    torch.cuda.synchronize()
+    assert int((st != 0).sum().item()) == 0
+    assert torch.equal(back, src.arena)
