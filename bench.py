@@ -714,11 +714,13 @@ def run_single(args, lzo, synth):
     return result, errors
 
 
-def run_others(args, torch, dist, lzo, synth, shard, dev, rank, backend):
-    """C5 (configs[4]: the append-file loop) and C4 (configs[3] per GPU: 131,072
-    mixed 4-256 KiB blocks, decode and compress kernels) measured in the
-    same run as the C3 headline, so the driver's record holds them too.  Each
-    is reported beside the headline, never as its value."""
+def run_others(args, torch, dist, lzo, synth, shard, dev, world, rank, backend):
+    """C5 (configs[4]: the append-file loop, N = 1 only) and C4 (configs[3]:
+    131,072 mixed 4-256 KiB blocks per GPU, global block i on rank i mod G, so
+    8 ranks hold the 1 M blocks; decode and compress kernels, whole-job rates)
+    measured in the same run as the C3 headline, so the driver's record holds
+    them too (its 1/2/4/8-GPU runs give the C4 curve).  Each is reported
+    beside the headline, never as its value."""
     import copy
     import gc
     out = {}
@@ -727,9 +729,10 @@ def run_others(args, torch, dist, lzo, synth, shard, dev, rank, backend):
     a = copy.copy(args)
     a.workload, a.steps, a.warmup = "c5", 10, 1
     try:
-        r, e = run_c5(a, rank)
-        out["c5"] = dict(r["e2e"], metric=r["metric"], workload=r["config"]["workload"], errors=e)
-        out["c5"].pop("xnet", None)
+        if world == 1:
+            r, e = run_c5(a, rank)
+            out["c5"] = dict(r["e2e"], metric=r["metric"], workload=r["config"]["workload"], errors=e)
+            out["c5"].pop("xnet", None)
     except Exception as exc:
         out["c5"] = {"error": repr(exc), "errors": 1}
     gc.collect()
@@ -737,11 +740,13 @@ def run_others(args, torch, dist, lzo, synth, shard, dev, rank, backend):
     a = copy.copy(args)
     a.workload, a.steps, a.warmup, a.compress_steps, a.no_cpu = "c4", 3, 1, 1, True
     try:
-        r, e = run_resident(a, torch, dist, lzo, synth, shard, dev, 1, rank, backend)
-        out["c4"] = {"workload": r["config"]["workload"], "blocks": r["config"]["blocks_per_gpu"],
-                     "decompress_gibps": r["value"], "compress_kernel_gibps": r["compress_kernel_gibps"],
-                     "step_ms": r["step_ms"], "compression_ratio": r["config"]["compression_ratio"],
-                     "decode_roofline_frac": r["roofline"]["frac"], "errors": e}
+        r, e = run_resident(a, torch, dist, lzo, synth, shard, dev, world, rank, backend)
+        out["c4"] = {"workload": r["config"]["workload"], "n_gpus": world,
+                     "blocks_per_gpu": r["config"]["blocks_per_gpu"],
+                     "decompress_gibps": r["value"],             # all ranks' blocks / max rank time
+                     "compress_kernel_gibps_rank0": r["compress_kernel_gibps"],
+                     "step_ms_rank0": r["step_ms"], "compression_ratio": r["config"]["compression_ratio"],
+                     "decode_roofline_frac_rank0": r["roofline"]["frac"], "errors": e}
     except Exception as exc:                       # (reported, never hides the headline)
         out["c4"] = {"error": repr(exc), "errors": 1}
     return out
@@ -783,9 +788,9 @@ def main():
     else:
         result, errors = run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank,
                                       backend)
-        if args.workload == "c3" and world == 1 and not args.no_others:
-            result["other_configs"] = run_others(args, torch, dist, lzo, synth, shard, dev, rank,
-                                                 backend)
+        if args.workload == "c3" and not args.no_others:
+            result["other_configs"] = run_others(args, torch, dist, lzo, synth, shard, dev, world,
+                                                 rank, backend)
             errors += sum(o.get("errors", 1) for o in result["other_configs"].values())
     if rank == 0:
         print(json.dumps(result), flush=True)
