@@ -100,9 +100,15 @@ typedef EncLdsT<false> EncLds;
 static_assert(sizeof(EncLdsT<false>) * 4 <= 160 * 1024, "LDS budget");
 static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budget");
 
-// Dictionary access: S.dict (LDS) or the workgroup's region in global memory
-// (non-temporal loads: served by L2, so a load sees this wave's earlier
-// dictionary stores).
+// Dictionary access: S.dict (LDS) or the workgroup's region in global memory.
+// Probes are agent-scope relaxed atomic loads (global_load_ushort sc1): served
+// by L2, never by a stale vector-L1 line, so a probe sees this wave's earlier
+// dictionary stores.  Non-temporal probes (round 2 until the last build) are as
+// exact but mark the lines evict-first in L2: the 512 dictionaries of an XCD then
+// miss L2 far more often, and the C3 compress kernel took 2.23 instead of 1.84 ms.
+#ifndef POM_DICT_LOAD
+#define POM_DICT_LOAD 2                         // probe loads: 0 non-temporal, 1 plain, 2 agent-scope atomic
+#endif
 typedef __attribute__((address_space(1))) uint16_t gu16;
 template <bool GD>
 struct Dict {
@@ -110,8 +116,15 @@ struct Dict {
     gu16* g;
     __device__ __forceinline__ uint32_t get(uint32_t slot) const
     {
-        if (GD)
+        if (GD) {
+#if POM_DICT_LOAD == 1
+            return g[slot];
+#elif POM_DICT_LOAD == 2
+            return __hip_atomic_load((uint16_t*)(g + slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
             return __builtin_nontemporal_load(g + slot);
+#endif
+        }
         return lds[slot];
     }
     __device__ __forceinline__ void put(uint32_t slot, uint32_t v) const
@@ -125,7 +138,7 @@ struct Dict {
     __device__ __forceinline__ uint32_t get2(uint32_t i) const
     {
         if (GD)
-            return __builtin_nontemporal_load((__attribute__((address_space(1))) uint32_t*)g + i);
+            return __hip_atomic_load((uint32_t*)g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return ((uint32_t*)lds)[i];
     }
     __device__ __forceinline__ void put2(uint32_t i, uint32_t v) const
