@@ -593,6 +593,12 @@ typedef __attribute__((address_space(1))) const uint32_t gdword;
 // served (the vector L1 is not coherent with the writer wave's stores).
 // Address-space-1 pointers keep these global_load (vmcnt only), not flat_load
 // (which also waits on lgkmcnt and so on every outstanding LDS access).
+#ifndef POM_OUT_NT
+#define POM_OUT_NT 0                             // writer: non-temporal output stores
+#endif
+#ifndef POM_FAR_SC1
+#define POM_FAR_SC1 0                            // far reads: agent-scope loads instead of non-temporal
+#endif
 template <bool NT>
 __device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
 {
@@ -625,7 +631,8 @@ __device__ __forceinline__ uint4 global_read16(const uint8_t* p, uint32_t lo, ui
     for (uint32_t i = 0; i < 5; i++) {
         // aligned dword i holds bytes 4i - sh .. 4i + 3 - sh of the span
         const bool use = 4 * i < hi + sh && 4 * i + 4 > lo + sh;
-        w[i] = use ? __builtin_nontemporal_load(q + i) : 0u;
+        w[i] = use ? (POM_FAR_SC1 ? __hip_atomic_load((uint32_t*)(q + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : __builtin_nontemporal_load(q + i)) : 0u;
     }
     uint4 v;
     v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
@@ -777,7 +784,10 @@ __device__ __forceinline__ uint32_t writer_duty(FastLds& S, uint8_t* out, uint32
         if (x + 16 <= end) {
             const uint32_t i = x & kRingMask;
             const uint4 v = *(const uint4*)&S.ring[i >> 2];
-            *(uint4*)(out + x) = v;
+            if (POM_OUT_NT)
+                __builtin_nontemporal_store((v4u32){v.x, v.y, v.z, v.w}, (v4u32*)(out + x));
+            else
+                *(uint4*)(out + x) = v;
         } else if (x < end) {
             for (uint32_t q = 0; x + q < end; q++)
                 out[x + q] = (uint8_t)ring_byte(S, x + q);

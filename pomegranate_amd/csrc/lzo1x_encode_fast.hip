@@ -106,6 +106,12 @@ static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budge
 // dictionary stores.  Non-temporal probes (round 2 until the last build) are as
 // exact but mark the lines evict-first in L2: the 512 dictionaries of an XCD then
 // miss L2 far more often, and the C3 compress kernel took 2.23 instead of 1.84 ms.
+#ifndef POM_CAND_AUX
+#define POM_CAND_AUX 0                          // cache policy of the candidate loads (buffer aux bits)
+#endif
+#ifndef POM_PW_AUX
+#define POM_PW_AUX 0                            // cache policy of the probe-word loads
+#endif
 #ifndef POM_DICT_LOAD
 #define POM_DICT_LOAD 2                         // probe loads: 0 non-temporal, 1 plain, 2 agent-scope atomic
 #endif
@@ -207,7 +213,7 @@ __device__ __forceinline__ BlockSrc block_src(const uint8_t* in, uint32_t n)
 // NW little-endian dwords of the block starting at byte pos (any alignment).
 // Aligned dwords lying wholly past the block's last byte read as 0: callers
 // cap every comparison at the block end.
-template <int NW>
+template <int NW, int AUX = 0>
 __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_t (&w)[NW])
 {
     const uint32_t a = pos + B.sh0;
@@ -215,7 +221,7 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
     uint32_t r[NW + 1];
 #pragma unroll
     for (int i = 0; i <= NW; i++)
-        r[i] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, a0 + 4 * i, 0, 0);
+        r[i] = __builtin_amdgcn_raw_buffer_load_b32(B.rs, a0 + 4 * i, 0, AUX);
 #pragma unroll
     for (int i = 0; i < NW; i++)
         w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], a & 3u);
@@ -599,8 +605,8 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // checked, no memory request; the secondary candidate is only
             // ever compared when the primary one is more than M2_MAX_OFFSET
             // back, lib/minilzo.c:2946-2949)
-            load_at<kCmpW>(B, v1 ? w1 : kFarPos, c1w);
-            load_at<kCmpW>(B, v2 && p - w1 > kM2MaxOffset ? w2 : kFarPos, c2w);
+            load_at<kCmpW, POM_CAND_AUX>(B, v1 ? w1 : kFarPos, c1w);
+            load_at<kCmpW, POM_CAND_AUX>(B, v2 && p - w1 > kM2MaxOffset ? w2 : kFarPos, c2w);
 #else
             load_at<kCmpW>(B, w1, c1w);
             load_at<kCmpW>(B, w2, c2w);
@@ -742,7 +748,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
 
             uint32_t npw[kCmpW];
-            load_at<kCmpW>(B, ip + end + l, npw);
+            load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
 
             ESTAMP(EP_CLAIM);
             // ---- tokens for the matches before the cut ------------------------
