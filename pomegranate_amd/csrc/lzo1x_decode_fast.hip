@@ -596,8 +596,11 @@ typedef __attribute__((address_space(1))) const uint32_t gdword;
 #ifndef POM_OUT_NT
 #define POM_OUT_NT 0                             // writer: non-temporal output stores
 #endif
+#ifndef POM_SRC_SC1
+#define POM_SRC_SC1 1                            // source-buffer loads: agent-scope (L2-allocating) instead of non-temporal
+#endif
 #ifndef POM_FAR_SC1
-#define POM_FAR_SC1 0                            // far reads: agent-scope loads instead of non-temporal
+#define POM_FAR_SC1 1                            // far reads: agent-scope (L2-allocating) loads instead of non-temporal
 #endif
 template <bool NT>
 __device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
@@ -1220,8 +1223,13 @@ __device__ __forceinline__ SrcCopy src_issue(FastLds& S, const Blk& k, uint32_t 
         w0[i] = S.ring[(a & kRingMask) >> 2];
         w1[i] = 0;
         if (hbm[i]) {
+#if POM_SRC_SC1
+            w0[i] = __hip_atomic_load((uint32_t*)qa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w1[i] = __hip_atomic_load((uint32_t*)qb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
             w0[i] = __builtin_nontemporal_load((gdword*)qa);
             w1[i] = __builtin_nontemporal_load((gdword*)qb);
+#endif
         }
     }
     // (funnels in src_commit: the loads' latency hides under forwarding)
