@@ -1,5 +1,6 @@
 set -u
-OUT=gpurun_out/prof_r02e
+TAG=${1:-r02e}
+OUT=gpurun_out/prof_${TAG}_c4c5
 mkdir -p $OUT
 export TMPDIR=/tmp
 python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || exit 1
