@@ -112,6 +112,12 @@ static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budge
 #ifndef POM_PW_AUX
 #define POM_PW_AUX 0                            // cache policy of the probe-word loads
 #endif
+#ifndef POM_ENC_PRIO
+#define POM_ENC_PRIO 1                          // one-wave kernel: wave priority by input bytes left
+#endif
+#ifndef POM_ENC_PRIO_STEP
+#define POM_ENC_PRIO_STEP 8192
+#endif
 #ifndef POM_DICT_LOAD
 #define POM_DICT_LOAD 2                         // probe loads: 0 non-temporal, 1 plain, 2 agent-scope atomic
 #endif
@@ -559,6 +565,21 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
         for (;;) {
             if (STAMPS)
                 acc[EC_WINDOWS] += 1;
+#if POM_ENC_PRIO
+            if (FUSED) {
+                // (one-wave kernel) blocks that are behind (more input left) get
+                // the issue slots first, so the workgroups of a CU finish together
+                const uint32_t left = n - ip, st = POM_ENC_PRIO_STEP;
+                const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
+                                                                  : left >= st ? 1u : 0u);
+                switch (q) {
+                case 3: __builtin_amdgcn_s_setprio(3); break;
+                case 2: __builtin_amdgcn_s_setprio(2); break;
+                case 1: __builtin_amdgcn_s_setprio(1); break;
+                default: __builtin_amdgcn_s_setprio(0); break;
+                }
+            }
+#endif
             if (ip + kWave - base >= 0xFFFFu) {     // this window's positions would not fit
                 const uint32_t nb = (ip - (kM4MaxOffset + 1)) / kRebase * kRebase;
                 const uint32_t delta = nb - base;
