@@ -299,13 +299,14 @@ struct Emitter {
     uint32_t ct;                                     // tokens consumed
     uint32_t pos;                                    // input covered by the tokens so far
     bool poisoned;                                   // a token the parse cannot have meant
+    bool prio;                                       // (one-wave kernel) wave priority by input left
     uint32_t* olen;                                  // out_len / status / block of drain(prod)
     int32_t* ost;
     uint32_t blk;
 
     __device__ __forceinline__ Emitter(EncLdsT<GD>& S_, const uint8_t* in, uint32_t n_, uint8_t* out,
                                        uint32_t cap)
-        : S(S_), B(block_src(in, n_)), n(n_), ct(0), pos(0), poisoned(false), olen(nullptr),
+        : S(S_), B(block_src(in, n_)), n(n_), ct(0), pos(0), poisoned(false), prio(false), olen(nullptr),
           ost(nullptr), blk(0)
     {
         e.in = in;
@@ -566,9 +567,10 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             if (STAMPS)
                 acc[EC_WINDOWS] += 1;
 #if POM_ENC_PRIO
-            if (FUSED) {
-                // (one-wave kernel) blocks that are behind (more input left) get
-                // the issue slots first, so the workgroups of a CU finish together
+            if (FUSED && E->prio) {
+                // (one-wave kernel, one block per workgroup) blocks that are behind
+                // (more input left) get the issue slots first, so the workgroups of
+                // a CU finish together
                 const uint32_t left = n - ip, st = POM_ENC_PRIO_STEP;
                 const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
                                                                   : left >= st ? 1u : 0u);
@@ -1016,6 +1018,7 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
         E.olen = out_len;
         E.ost = status;
         E.blk = b;
+        E.prio = !dyn;                               // (block tickets: mixed sizes, no priority)
         uint64_t acc[EP_N];
         parse_wave<false, true, true>(S, D, in, n, l, acc, &E);
         wave_order();
