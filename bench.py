@@ -328,7 +328,7 @@ class Resident:
         self.fallback_blocks = int(self.scratch[:4].view(torch.int32).item())
 
     def compress(self):
-        self.lzo.compress_dev(self.src, self.zdst, self.zlen, self.zst, self.cscratch)
+        self.lzo.compress_dev(self.src, self.zdst, self.zlen, self.zst, scratch=self.cscratch)
 
     def decompress(self):
         self.lzo.decompress_dev(self.zsrc, self.odst, self.olen, self.ost, self.scratch)
@@ -379,6 +379,11 @@ class Resident:
         return plain, comps
 
 
+def dist_on(dist) -> bool:
+    """A process group exists (torchrun ranks; the RCCL test at world size 1)."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def timed(torch, dist, world, stream, phases, steps, warmup):
     """Wall time of `steps` steps (each: the phases in order), bracketed by a
     barrier and a synchronize on both sides, and the average HIP-event time of
@@ -386,7 +391,7 @@ def timed(torch, dist, world, stream, phases, steps, warmup):
     for _ in range(warmup):
         for f in phases:
             f()
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(phases) + 1)]
@@ -398,7 +403,7 @@ def timed(torch, dist, world, stream, phases, steps, warmup):
             f()
             evs[k][i + 1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     wall = time.perf_counter() - t0
     per = [sum(evs[k][i].elapsed_time(evs[k][i + 1]) for k in range(steps)) / 1e3 / max(steps, 1)
@@ -473,7 +478,7 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
         dec_wall, t_d2 = wall, t_d
         _, (t_c,) = timed(torch, dist, world, stream, [R.compress], args.compress_steps, 1)
         errors += int((R.ost != 0).sum().item()) + int((R.zst != 0).sum().item())
-    if world > 1:
+    if dist_on(dist):
         errors, wall = shard.completion_barrier(dist, dev, errors, wall)
         _, dec_wall = shard.completion_barrier(dist, dev, 0, dec_wall)
         tot = torch.tensor([n_bytes, z_bytes], dtype=torch.float64,

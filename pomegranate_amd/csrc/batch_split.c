@@ -127,3 +127,26 @@ int pom_run_devices(int ndev, pom_dev_fn fn, void *arg)
     free(started);
     return rc;
 }
+
+/* A device listed twice is used once: two helper threads on one device would
+ * share (and reallocate under each other) the calling thread's slots. */
+int pom_parse_devices(const char *list, int count, int max_dev, int *devs)
+{
+    int n = 0;
+    unsigned long long seen = 0;
+    const char *p = list;
+    if (max_dev > 64)
+        max_dev = 64;
+    while (*p && n < max_dev) {
+        char *q;
+        const long v = strtol(p, &q, 10);
+        if (q == p)
+            break;
+        if (v >= 0 && v < count && v < max_dev && !(seen & (1ull << v))) {
+            seen |= 1ull << v;
+            devs[n++] = (int)v;
+        }
+        p = *q == ',' ? q + 1 : q;
+    }
+    return n;
+}

@@ -42,6 +42,10 @@ size_t pom_chunk_end(const size_t *ids, size_t from, size_t n, const size_t *cos
 typedef int (*pom_dev_fn)(void *arg, int d);
 int pom_run_devices(int ndev, pom_dev_fn fn, void *arg);
 
+/* POM_LZO_DEVICES parsing: device ids in [0, min(count, max_dev)) from a
+ * comma list, in order, each at most once.  Returns how many were stored. */
+int pom_parse_devices(const char *list, int count, int max_dev, int *devs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,7 @@
 #include <sys/uio.h>
 #include <unistd.h>
 
+#include "io_util.h"
 #include "lzo_mi355x.h"
 #include "minilzo.h"
 #include "pom_itb.h"
@@ -277,24 +278,7 @@ int pom_abuf_append_batch(struct pom_abuf *ab, const void *const *recs, const si
                     iov[j].iov_len = len[j0 + j];
                     want += len[j0 + j];
                 }
-                size_t got = 0;
-                while (got < want) {                 /* (a short write resumes) */
-                    struct iovec *v = iov;
-                    size_t nv = m, skip = got;
-                    while (skip >= v->iov_len) {
-                        skip -= v->iov_len;
-                        v++;
-                        nv--;
-                    }
-                    v->iov_base = (uint8_t *)v->iov_base + skip;
-                    v->iov_len -= skip;
-                    const ssize_t w = pwritev(ab->fd, v, (int)nv, (off_t)(fo + got));
-                    if (w <= 0) {
-                        rc = w < 0 ? -errno : -EIO;
-                        break;
-                    }
-                    got += (size_t)w;
-                }
+                rc = pom_pwritev_all(ab->fd, iov, (int)m, (off_t)fo, NULL);
                 fo += want;
             }
             if (rc)

@@ -672,23 +672,15 @@ static int dev_run(void *arg, int d)
 }
 
 /* Devices a host batch may use: POM_LZO_DEVICES ("0,2,3"; default every
- * visible device).  Processes that run one rank per GPU set it to their own. */
+ * visible device; parsed by pom_parse_devices, duplicates dropped).
+ * Processes that run one rank per GPU set it to their own. */
 static int batch_devices(int *devs)
 {
     const int count = lzo_mi355x_device_count();
     int n = 0;
     const char *e = getenv("POM_LZO_DEVICES");
     if (e && *e) {
-        const char *p = e;
-        while (*p && n < kMaxDev) {
-            char *q;
-            const long v = strtol(p, &q, 10);
-            if (q == p)
-                break;
-            if (v >= 0 && v < count && v < kMaxDev)
-                devs[n++] = (int)v;
-            p = *q == ',' ? q + 1 : q;
-        }
+        n = pom_parse_devices(e, count, kMaxDev, devs);
     } else {
         for (int d = 0; d < count && d < kMaxDev; d++)
             devs[n++] = d;

@@ -233,21 +233,30 @@ def _stream_handle(torch, stream=None) -> int:
     return int(s.cuda_stream)
 
 
-def compress_dev(src: DeviceBatch, dst: DeviceBatch, out_len, status, scratch="auto",
-                 stream=None) -> None:
+def compress_dev(src: DeviceBatch, dst: DeviceBatch, out_len, status, stream=None, *,
+                 scratch="auto") -> None:
     """Enqueue LZO1X-1 compression of every block of src into dst (dst.length = capacity).
 
-    scratch: device tensor of compress_scratch_bytes(nblocks) bytes for the
-    per-workgroup match dictionaries (16 blocks per CU parse at once), None for
-    LDS dictionaries (4 per CU), or "auto" to allocate one for this call."""
+    stream: the HIP stream (torch.cuda.Stream) to enqueue on; default the current one.
+    scratch (keyword only): device tensor of compress_scratch_bytes(nblocks) bytes
+    for the per-workgroup match dictionaries (16 blocks per CU parse at once),
+    None for LDS dictionaries (4 per CU), or "auto" to allocate one for this
+    call.  An "auto" tensor is allocated on, and recorded against, the stream
+    the kernel runs on, so the caching allocator cannot hand its memory to
+    another tensor while the encoder still uses it."""
     import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
     if isinstance(scratch, str):
+        if scratch != "auto":
+            raise ValueError(f"scratch: a tensor, None or 'auto', not {scratch!r}")
         nbytes = compress_scratch_bytes(src.nblocks)
-        scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=src.arena.device)
+        with torch.cuda.stream(s):
+            scratch = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=src.arena.device)
+        scratch.record_stream(s)
     rc = load().lzo_mi355x_compress_dev(
         _ptr(src.arena), _ptr(src.off), _ptr(src.length), _ptr(dst.arena), _ptr(dst.off),
         _ptr(dst.length), _ptr(out_len), _ptr(status), src.nblocks,
-        _ptr(scratch) if scratch is not None else None, _stream_handle(torch, stream))
+        _ptr(scratch) if scratch is not None else None, int(s.cuda_stream))
     if rc != 0:
         raise RuntimeError("lzo_mi355x_compress_dev launch failed")
 

@@ -63,3 +63,53 @@ int mock_batch(size_t n, const uint8_t *const *src, const size_t *len, uint8_t *
     free(cost);
     return rc;
 }
+
+/* POM_LZO_DEVICES parsing (batch_split.c), exposed for tests/test_split.py */
+int mock_parse_devices(const char *list, int count, int max_dev, int *devs)
+{
+    return pom_parse_devices(list, count, max_dev, devs);
+}
+
+/* pom_pwritev_all (io_util.c) under a writer that writes at most `g_step`
+ * bytes per call, cut inside iovecs, and fails every third call with EINTR. */
+#include <errno.h>
+#include <string.h>
+#include <sys/uio.h>
+#include "io_util.h"
+
+static size_t g_step;
+static unsigned g_calls;
+static uint8_t *g_file;
+
+static ssize_t short_pwritev(int fd, const struct iovec *iov, int n, off_t off)
+{
+    (void)fd;
+    if (++g_calls % 3 == 0) {
+        errno = EINTR;
+        return -1;
+    }
+    size_t left = g_step, w = 0;
+    for (int i = 0; i < n && left; i++) {
+        size_t k = iov[i].iov_len < left ? iov[i].iov_len : left;
+        memcpy(g_file + off + w, iov[i].iov_base, k);
+        w += k;
+        left -= k;
+    }
+    return (ssize_t)w;
+}
+
+int mock_pwritev_all(uint8_t *file, const uint8_t *const *bufs, const size_t *lens, int n,
+                     size_t step, long off)
+{
+    struct iovec iov[64];
+    if (n > 64)
+        return -1;
+    for (int i = 0; i < n; i++) {
+        iov[i].iov_base = (void *)bufs[i];
+        iov[i].iov_len = lens[i];
+    }
+    g_step = step;
+    g_calls = 0;
+    g_file = file;
+    return pom_pwritev_all(-1, iov, n, (off_t)off, short_pwritev);
+}

@@ -143,3 +143,54 @@ def test_two_ranks_share_the_gpu_codec(oracle):
     for rank, mine, _, comps in res:
         for i, z in zip(mine, comps):
             assert z == oracle.compress(synth.block(synth.ITB, 7000 + i, 4096 + 1024 * (i % 13)))
+
+
+def _rccl_worker(port, q):
+    """World size 1 over RCCL exactly as bench.py:main initialises it (nccl
+    backend, device_id), then the completion barrier on device tensors and a
+    small C4 share through bench.run_resident, whose barriers and all-reduces
+    now run over RCCL."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"] = "0"
+    os.environ["WORLD_SIZE"] = "1"
+    try:
+        import argparse
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        from pomegranate_amd import lzo
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        try:
+            assert dist.get_backend() == "nccl"
+            barrier = shard.completion_barrier(dist, dev, 3, 1.25)
+            args = argparse.Namespace(workload="c4", c4_blocks=256, steps=2, warmup=1,
+                                      compress_steps=1, model="itb", block_bytes=65536,
+                                      blocks=4096, no_cpu=True, cpu_seconds=0.0)
+            lzo.load()
+            res, errors = bench.run_resident(args, torch, dist, lzo, synth, shard, dev, 1, 0,
+                                             "nccl")
+            q.put(("ok", barrier, errors, res["value"], res["config"]["blocks_per_gpu"]))
+        finally:
+            dist.destroy_process_group()
+    except Exception as exc:                     # reported to the parent
+        q.put(("error", repr(exc)))
+
+
+@pytest.mark.gpu
+def test_rccl_world_one_barrier_and_c4_share():
+    """the RCCL (nccl backend) path runs once on a GPU
+    before any scaling run needs it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[0] == "ok", res
+    _, barrier, errors, value, nblocks = res
+    assert barrier == (3, 1.25)
+    assert errors == 0 and nblocks == 256 and value > 0
+    assert p.exitcode == 0

@@ -131,3 +131,42 @@ def test_split_concurrent_callers(mock):
     for t in th:
         t.join()
     assert not errs
+
+
+@pytest.mark.parametrize("spec,count,want", [
+    ("0,0", 8, [0]),                      # duplicate: one helper thread per device
+    ("1,0,1,2,0", 4, [1, 0, 2]),
+    ("3,9,2", 4, [3, 2]),                 # out of range dropped
+    ("", 4, []),
+    ("2,,1", 4, [2]),                     # parsing stops at a malformed entry
+])
+def test_parse_devices_drops_duplicates(mock, spec, count, want):
+    """POM_LZO_DEVICES (lzo_host.c batch_devices): a device listed twice must
+    not get two helper threads sharing the caller's slots."""
+    mock.mock_parse_devices.restype = ctypes.c_int
+    mock.mock_parse_devices.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p]
+    devs = (ctypes.c_int * 16)()
+    n = mock.mock_parse_devices(spec.encode(), count, 16, devs)
+    assert list(devs[:n]) == want
+
+
+@pytest.mark.parametrize("step", [1, 3, 7, 100, 1 << 20])
+def test_pwritev_resumes_short_writes(mock, step):
+    """MDSL append file (itb_codec.c, mdsl/storage.c:455-519): a gathered
+    write that the kernel cuts short, possibly twice inside one iovec, or
+    interrupts with EINTR, must still land every byte once, in order."""
+    rng = np.random.default_rng(step)
+    lens = [0, 5, 17, 0, 1, 64, 3, 250]
+    bufs = [ctypes.create_string_buffer(rng.integers(0, 256, n, dtype=np.uint8).tobytes(), max(n, 1))
+            for n in lens]
+    file = ctypes.create_string_buffer(sum(lens) + 40)
+    mock.mock_pwritev_all.restype = ctypes.c_int
+    mock.mock_pwritev_all.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int, ctypes.c_size_t, ctypes.c_long]
+    arr = (ctypes.c_void_p * len(bufs))(*[ctypes.cast(b, ctypes.c_void_p).value for b in bufs])
+    ln = (ctypes.c_size_t * len(lens))(*lens)
+    assert mock.mock_pwritev_all(file, arr, ln, len(lens), step, 40) == 0
+    want = b"".join(b.raw[:n] for b, n in zip(bufs, lens))
+    assert file.raw[40:40 + len(want)] == want
+    assert file.raw[:40] == b"\0" * 40
