@@ -1,0 +1,811 @@
+// lzo1x_decode_win.hip -- the windowed LZO1X decoder for MI355X (gfx950).
+//
+// One workgroup of 8 waves per block; the block's last 64 KiB of output stay
+// resident in an LDS ring (every LZO1X match distance, <= 0xBFFF, reaches into
+// it), so a block never reads its own output back from HBM.  Two workgroups
+// share a CU (80 KB of LDS each).  The block is decoded as an alternation of
+//
+//  * PIECES of compressed input (kZH = 2 KiB, staged in one half of a 4 KiB
+//    LDS ring): 128 parse lanes, each owning a 16-byte segment, find the
+//    instruction starts of the LZO1X grammar (lib/minilzo.c:3308-3699,
+//    SURVEY.md Appendix A.2) as a state machine over (position, state):
+//      - every lane walks speculatively from 16 bytes before its segment and
+//        keeps the starts it visits inside the segment as per-state bitmaps;
+//      - a lane whose true entry (its predecessor's exit) is not one of its
+//        speculative starts walks exactly from it until it lands on one; the
+//        exits settle by Jacobi iteration over the lanes (one barrier each,
+//        about two rounds per piece on ITB streams);
+//      - a counting walk, a scan over the lanes, and an emitting walk write
+//        the piece's ops (output start, literal zin offset or match distance)
+//        to an LDS op table of kOpCap entries;
+//  * WINDOWS of output (kW = 4 KiB, lane = 8 output bytes): every output byte
+//    gets a source pointer, encoded as e = B - t for a source at output
+//    position t (B = window end - 1) or kLitBase + zin offset for a literal
+//    byte.  Matches that overlap themselves (distance d < length) are reduced
+//    to the last period before max(op start, window start).  A source inside
+//    the window (e <= T) is followed through the window's pointer table
+//    (e = tab[W - 1 - e], with write-back, so chains shorten as they are
+//    walked) until it is a literal or lies before the window.  Then every
+//    byte is one independent LDS gather, written to the ring and to HBM.
+//    The pointer table (2 bytes per window byte) lives in the ring itself,
+//    just past the window: those slots hold output older than any match can
+//    reach (kW <= 8 KiB).
+//
+// Blocks it does not finish exactly (malformed input, lookbehind/capacity
+// errors, instructions longer than a piece, misaligned destinations) are
+// appended to the fallback list for lzo1x_decode_exact_kernel
+// (lzo1x_kernels.hip), which produces the reference's output and LZO_E_* code
+// bit for bit.  The algorithm was checked first as a sequential C model
+// (scripts/dbg/win_model.c) against the oracle.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lzo_mi355x_kernels.h"
+
+namespace {
+
+constexpr uint32_t kWave = 64;
+constexpr uint32_t kNT = 512;                    // threads per workgroup (8 waves)
+constexpr uint32_t kW = 4096;                    // window bytes (8 per thread)
+constexpr uint32_t kZH = 2048;                   // compressed bytes per piece
+constexpr uint32_t kZR = 2 * kZH;                // zin ring (two pieces)
+constexpr uint32_t kOpCap = 1024;                // ops held at once
+constexpr uint32_t kG = 16;                      // parse segment bytes
+constexpr uint32_t kNPL = kZH / kG;              // parse lanes (waves 0-1)
+constexpr uint32_t kLook = 16;                   // speculative lead-in
+constexpr uint32_t kLitBase = 65536u - kZR;      // e >= kLitBase: literal at zin[e - kLitBase]
+constexpr uint32_t kLitF = 0x80000000u;
+constexpr int32_t kFallback = 0x7FFF0001;
+static_assert(kW * 8 == kNT * 64, "window: 8 bytes per thread");
+static_assert(2 * kW <= 65536u - 0xBFFFu - 1u, "pointer table slots must be dead ring slots");
+static_assert(0xBFFFu + kW < kLitBase, "e encoding: match pointers below literal ones");
+static_assert(kNPL == 2 * kWave, "two parse waves");
+
+enum : uint32_t { ST_A = 0, ST_B = 1, ST_C = 2, ST_F = 3 };
+enum : uint32_t { TK_EOF = 1, TK_BAD = 2, TK_CUT = 4 };
+// piece results
+enum : uint32_t { PR_OK = 0, PR_EOF = 1, PR_FULL = 2, PR_REFUSE = 3 };
+// control words
+enum : uint32_t {
+    C_REFUSE = 0, C_STOPLANE, C_SPOS, C_SST, C_SKIND, C_CUTLANE, C_CUTPOS, C_CUTST, C_CUTOPS,
+    C_CUTBYTES, C_TOPS, C_TBYTES, C_N = 16
+};
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+struct __attribute__((aligned(16))) WinLds {
+    uint8_t ring[65536];
+    uint32_t zin[kZR / 4 + 4];                   // + pad: 4-byte reads past the end
+    uint32_t opp[kOpCap + 4];                    // op output start; opp[nops] = end
+    uint32_t ops[kOpCap];                        // kLitF | zin offset, or match distance
+    uint32_t bmap[2][kW / 32];                   // op starts of the window
+    uint32_t ex[2][kNPL];                        // parse-lane exits (rel pos << 2 | state)
+    uint32_t wsum[4];
+    uint32_t cnt[4];
+    uint32_t ctl[C_N];
+};
+static_assert(sizeof(WinLds) <= 81920, "two workgroups per CU");
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Inclusive prefix sum over the wave (DPP row shifts, then row totals).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31),
+                   r2 = __builtin_amdgcn_readlane(v, 47);
+    const uint32_t row = lane_id() >> 4;
+    v += (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+
+// ---- compressed input (staged piece) --------------------------------------
+struct Piece {
+    uint32_t I;          // input position of zin byte zb
+    uint32_t zb;         // byte offset of the piece's half in zin
+    uint32_t lim;        // min(z, I + kZH): bytes below are real staged input
+    uint32_t z;
+    bool lim_is_z;       // the piece holds the end of the input
+};
+
+__device__ __forceinline__ uint32_t zbyte(const WinLds& L, uint32_t off)
+{
+    return (L.zin[off >> 2] >> (8u * (off & 3u))) & 0xFFu;
+}
+
+struct Tok {
+    uint32_t pos, st;    // next instruction start
+    uint32_t aL, aS;     // op A: length, source (kLitF | input pos, or distance)
+    uint32_t bL, bS;     // op B: trailing literals (bL == 0: none)
+    uint32_t fl;         // TK_*
+};
+
+// One instruction at (pos, st), pos < k.lim, general form (long length
+// extensions).  Bytes at or past k.lim read as 0; the caller's flag logic
+// (tok_flags) classifies the instruction by where it ends.
+__device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t pos, uint32_t st)
+{
+    Tok r;
+    r.aL = r.bL = r.aS = r.bS = 0;
+    r.fl = 0;
+    uint32_t far = 0;    // furthest byte read + 1
+    auto rd = [&](uint32_t p) -> uint32_t {
+        far = p + 1 > far ? p + 1 : far;
+        return p < k.lim ? zbyte(L, k.zb + (p - k.I)) : 0u;
+    };
+    auto ext = [&](uint32_t& p, uint32_t base) -> uint32_t {
+        uint32_t v = 0;
+        while (p < k.lim && rd(p) == 0) {
+            v += 255;
+            p++;
+        }
+        v += base + rd(p);
+        p++;
+        return v;
+    };
+    uint32_t t = rd(pos);
+    if (st == ST_F) {
+        if (t > 17) {
+            const uint32_t n = t - 17;
+            r.aL = n;
+            r.aS = kLitF | (pos + 1);
+            r.pos = pos + 1 + n;
+            r.st = n < 4 ? ST_C : ST_B;
+            goto done;
+        }
+        st = ST_A;
+    }
+    {
+        uint32_t Ln, d;
+        if (t < 16 && st == ST_A) {
+            pos++;
+            if (t == 0)
+                t = ext(pos, 15);
+            r.aL = t + 3;
+            r.aS = kLitF | pos;
+            r.pos = pos + t + 3;
+            r.st = ST_B;
+            if (r.pos < pos)
+                r.pos = 0xFFFFFFF0u;             // wrapped: ends past anything
+            goto done;
+        }
+        if (t < 16) {
+            d = (st == ST_B ? 0x801u : 1u) + (t >> 2) + (rd(pos + 1) << 2);
+            Ln = st == ST_B ? 3u : 2u;
+            pos += 2;
+        } else if (t >= 64) {
+            d = 1 + ((t >> 2) & 7) + (rd(pos + 1) << 3);
+            Ln = (t >> 5) + 1;
+            pos += 2;
+        } else if (t >= 32) {
+            Ln = t & 31;
+            pos++;
+            if (Ln == 0)
+                Ln = ext(pos, 31);
+            Ln += 2;
+            d = 1 + ((rd(pos) | (rd(pos + 1) << 8)) >> 2);
+            pos += 2;
+        } else {
+            uint32_t dd = (t & 8) << 11;
+            Ln = t & 7;
+            pos++;
+            if (Ln == 0)
+                Ln = ext(pos, 7);
+            Ln += 2;
+            dd += (rd(pos) | (rd(pos + 1) << 8)) >> 2;
+            pos += 2;
+            if (dd == 0) {
+                r.fl = TK_EOF;
+                r.pos = pos;
+                r.st = ST_A;
+                goto done;
+            }
+            d = dd + 0x4000;
+        }
+        r.aL = Ln;
+        r.aS = d;
+        const uint32_t tl = rd(pos - 2) & 3;
+        if (tl) {
+            r.bL = tl;
+            r.bS = kLitF | pos;
+            pos += tl;
+            r.st = ST_C;
+        } else
+            r.st = ST_A;
+        r.pos = pos;
+    }
+done:
+    // classify by the furthest byte the instruction needs
+    {
+        const uint32_t need = far > r.pos ? far : r.pos;
+        if (need > k.lim)
+            r.fl = k.lim_is_z ? TK_BAD : TK_CUT;
+        else if ((r.fl & TK_EOF) && r.pos != k.z)
+            r.fl = TK_BAD;                       // EOF not at the end (INPUT_NOT_CONSUMED)
+    }
+    return r;
+}
+
+// Branch-free form for the common case: the instruction's fields lie in its
+// first 4 bytes (no 255-chunk length extension).  One zin round trip.
+__device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos, uint32_t st)
+{
+    const uint32_t off = k.zb + (pos - k.I);
+    const uint32_t lo = __builtin_amdgcn_alignbyte(L.zin[(off >> 2) + 1], L.zin[off >> 2], off & 3u);
+    const uint32_t t = lo & 0xFFu, b1 = __builtin_amdgcn_ubfe(lo, 8, 8);
+    const bool flit = st == ST_F && t > 17;
+    const uint32_t se = st == ST_F ? ST_A : st;
+    const bool lit = !flit && se == ST_A && t < 16;
+    const bool m1 = !flit && !lit && t < 16;
+    const bool m2 = !flit && t >= 64;
+    const bool m3 = !flit && t >= 32 && t < 64;
+    const bool m4 = !flit && t >= 16 && t < 32;
+    const bool ext = (lit && t == 0) || (m3 && (t & 31) == 0) || (m4 && (t & 7) == 0);
+    if (__builtin_expect(ext && b1 == 0, 0))
+        return tok_slow(L, k, pos, st);
+    const uint32_t e = ext ? 1u : 0u;
+    const uint32_t o16 = __builtin_amdgcn_ubfe(lo, 8u + 8u * e, 16);
+    const uint32_t dd4 = ((t & 8u) << 11) + (o16 >> 2);
+    const uint32_t used = (m1 || m2) ? 2u : 3u + e;
+    const uint32_t tl = __builtin_amdgcn_ubfe(lo, 8u * (used - 2u), 2);
+    const uint32_t nlit = flit ? t - 17 : (ext ? 15u + b1 : t) + 3u;
+    const uint32_t Ln = m1 ? (se == ST_B ? 3u : 2u)
+                      : m2 ? (t >> 5) + 1u
+                      : m3 ? (ext ? 31u + b1 : (t & 31u)) + 2u
+                           : (ext ? 7u + b1 : (t & 7u)) + 2u;
+    const uint32_t d = m1 ? (se == ST_B ? 0x801u : 1u) + (t >> 2) + (b1 << 2)
+                     : m2 ? 1u + ((t >> 2) & 7u) + (b1 << 3)
+                     : m3 ? 1u + (o16 >> 2) : dd4 + 0x4000u;
+    const bool eof = m4 && dd4 == 0;
+    const bool islit = flit || lit;
+    const uint32_t hdr = flit ? 1u : 1u + e;
+    Tok r;
+    r.aL = eof ? 0u : islit ? nlit : Ln;
+    r.aS = islit ? kLitF | (pos + hdr) : d;
+    r.bL = (islit || eof) ? 0u : tl;
+    r.bS = kLitF | (pos + used);
+    r.pos = islit ? pos + hdr + nlit : pos + used + (eof ? 0u : tl);
+    r.st = islit ? (flit && nlit < 4 ? ST_C : ST_B) : (tl && !eof ? ST_C : ST_A);
+    // the instruction (header, then literals) ends at r.pos
+    uint32_t fl = eof ? TK_EOF : 0u;
+    if (r.pos > k.lim)
+        fl = k.lim_is_z ? TK_BAD : TK_CUT;
+    else if (eof && r.pos != k.z)
+        fl = TK_BAD;
+    r.fl = fl;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t pack_pt(const Piece& k, uint32_t pos, uint32_t st) { return ((pos - k.I) << 2) | st; }
+
+// ---- block state ----------------------------------------------------------
+struct Blk {
+    const uint8_t* in;
+    uint8_t* out;
+    uint32_t z, cap;
+};
+
+// ---- piece parse ------------------------------------------------------------
+struct PieceOut {
+    uint32_t result;     // PR_*
+    uint32_t I, st;      // next piece entry
+    uint32_t nops, E;    // op count and output end after the piece
+};
+
+__device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t st_in, uint32_t nops,
+                                uint32_t E, uint32_t half)
+{
+    const uint32_t tid = threadIdx.x;
+    Piece k;
+    k.I = I;
+    k.zb = half * kZH;
+    k.z = blk.z;
+    k.lim = blk.z < I + kZH ? blk.z : I + kZH;
+    k.lim_is_z = blk.z <= I + kZH;
+
+    // stage: thread t loads input bytes I + 4t .. +3 (0 past z)
+    {
+        const uint32_t p = I + 4 * tid;
+        uint32_t v = 0;
+        if (p + 4 <= blk.z) {
+            const uint8_t* q = blk.in + p;
+            v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+        } else {
+            for (uint32_t i = 0; i < 4; i++)
+                if (p + i < blk.z)
+                    v |= (uint32_t)blk.in[p + i] << (8 * i);
+        }
+        L.zin[(k.zb >> 2) + tid] = v;
+        if (tid < C_N)
+            L.ctl[tid] = tid == C_STOPLANE || tid == C_CUTLANE ? kNone : 0u;
+        if (tid < 4)
+            L.cnt[tid] = 0;
+    }
+    __syncthreads();
+
+    const bool pl = tid < kNPL;
+    const uint32_t j = tid;
+    const uint32_t a = I + kG * j, b = a + kG;
+    const uint32_t entry0 = pack_pt(k, I, st_in);
+    uint32_t bm0 = 0, bm1 = 0, bm2 = 0, sx = 0;
+
+    // P1: speculative walks
+    if (pl) {
+        if (a >= k.lim && j) {
+            sx = pack_pt(k, b, ST_A);
+        } else {
+            uint32_t pos = j ? (a >= I + kLook ? a - kLook : I) : I;
+            uint32_t st = j ? (uint32_t)ST_A : st_in;
+            uint32_t restart = pos;
+            while (pos < b) {
+                const Tok t = tok(L, k, pos, st);
+                if (t.fl) {
+                    if (j == 0 || (t.fl & (TK_CUT | TK_EOF)))
+                        break;                   // stop point
+                    restart++;                   // impossible guess: start one byte later
+                    pos = restart;
+                    st = ST_A;
+                    bm0 = bm1 = bm2 = 0;
+                    continue;
+                }
+                if (pos >= a) {
+                    const uint32_t bit = 1u << (pos - a);
+                    const uint32_t s = st == ST_F ? ST_A : st;
+                    bm0 |= s == ST_A ? bit : 0u;
+                    bm1 |= s == ST_B ? bit : 0u;
+                    bm2 |= s == ST_C ? bit : 0u;
+                }
+                pos = t.pos;
+                st = t.st;
+            }
+            if (pos >= a && pos < b) {           // stopped inside: the stop point is a start
+                const uint32_t bit = 1u << (pos - a);
+                const uint32_t s = st == ST_F ? ST_A : st;
+                bm0 |= s == ST_A ? bit : 0u;
+                bm1 |= s == ST_B ? bit : 0u;
+                bm2 |= s == ST_C ? bit : 0u;
+            }
+            sx = pack_pt(k, pos, st);
+        }
+        L.ex[0][j] = sx;
+    }
+
+    auto in_bm = [&](uint32_t pos, uint32_t st) -> bool {
+        if (pos < a || pos >= b)
+            return false;
+        const uint32_t s = st == ST_F ? ST_A : st;
+        const uint32_t m = s == ST_A ? bm0 : s == ST_B ? bm1 : bm2;
+        return (m >> (pos - a)) & 1u;
+    };
+    // exit of this lane's segment from a true entry (packed)
+    auto exit_from = [&](uint32_t ent) -> uint32_t {
+        uint32_t pos = I + (ent >> 2), st = ent & 3u;
+        if (pos >= b)
+            return ent;
+        if (in_bm(pos, st))
+            return sx;
+        for (;;) {
+            const Tok t = tok(L, k, pos, st);
+            if (t.fl)
+                return pack_pt(k, pos, st);      // stop point
+            pos = t.pos;
+            st = t.st;
+            if (pos >= b)
+                return pack_pt(k, pos, st);
+            if (in_bm(pos, st))
+                return sx;
+        }
+    };
+
+    // P2: exits from true entries (Jacobi over the lanes, double-buffered)
+    uint32_t my_ent = kNone, my_ex = sx;
+    uint32_t it = 0;
+    for (;; it++) {
+        const uint32_t cur = it & 1u;
+        __syncthreads();
+        if (pl && j) {
+            const uint32_t ent = L.ex[cur][j - 1];
+            if (ent != my_ent) {
+                my_ent = ent;
+                const uint32_t nx = exit_from(ent);
+                if (nx != my_ex) {
+                    my_ex = nx;
+                    atomicAdd(&L.cnt[it % 3], 1u);
+                }
+            }
+        }
+        if (pl)
+            L.ex[cur ^ 1u][j] = my_ex;
+        if (tid == 0)
+            L.cnt[(it + 1) % 3] = 0;
+        __syncthreads();
+        if (L.cnt[it % 3] == 0)
+            break;
+    }
+    const uint32_t fin = (it + 1) & 1u;          // ex[fin] holds the settled exits
+    const uint32_t ent = pl ? (j ? L.ex[fin][j - 1] : entry0) : 0u;
+
+    // P3: count ops and bytes on the true path
+    uint32_t c_ops = 0, c_bytes = 0, skind = 0, spos = 0, sst = 0;
+    if (pl) {
+        uint32_t pos = I + (ent >> 2), st = ent & 3u;
+        while (pos < b) {
+            const Tok t = tok(L, k, pos, st);
+            if (t.fl) {
+                skind = t.fl;
+                spos = pos;
+                sst = st;
+                break;
+            }
+            c_ops += (t.aL ? 1u : 0u) + (t.bL ? 1u : 0u);
+            c_bytes += t.aL + t.bL;
+            pos = t.pos;
+            st = t.st;
+        }
+        if (skind)
+            atomicMin(&L.ctl[C_STOPLANE], j);
+    }
+    // scan over the two parse waves
+    const uint32_t wave = tid >> 6;
+    const uint32_t i_ops = wave_incl_scan(c_ops), i_bytes = wave_incl_scan(c_bytes);
+    if (tid == 63) {
+        L.wsum[0] = i_ops;
+        L.wsum[1] = i_bytes;
+    }
+    __syncthreads();
+    const uint32_t b_ops = i_ops - c_ops + (wave == 1 ? L.wsum[0] : 0u);
+    const uint32_t b_bytes = i_bytes - c_bytes + (wave == 1 ? L.wsum[1] : 0u);
+    const uint32_t stoplane = L.ctl[C_STOPLANE];
+    if (pl && j == stoplane) {
+        L.ctl[C_SPOS] = spos;
+        L.ctl[C_SST] = sst;
+        L.ctl[C_SKIND] = skind;
+    }
+    if (tid == kNPL - 1) {
+        L.ctl[C_TOPS] = b_ops + c_ops;
+        L.ctl[C_TBYTES] = b_bytes + c_bytes;
+    }
+
+    // P4: emit ops (stop at the op cap: that instruction starts the next piece)
+    const uint32_t avail = kOpCap - nops;
+    if (pl && c_ops && b_ops <= avail) {
+        uint32_t pos = I + (ent >> 2), st = ent & 3u;
+        uint32_t n = b_ops, outp = E + b_bytes;
+        while (pos < b) {
+            const Tok t = tok(L, k, pos, st);
+            if (t.fl)
+                break;
+            const uint32_t need = (t.aL ? 1u : 0u) + (t.bL ? 1u : 0u);
+            if (n + need > avail) {
+                L.ctl[C_CUTLANE] = j;
+                L.ctl[C_CUTPOS] = pos;
+                L.ctl[C_CUTST] = st;
+                L.ctl[C_CUTOPS] = n;
+                L.ctl[C_CUTBYTES] = outp - E;
+                break;
+            }
+            if (t.aL) {
+                L.opp[nops + n] = outp;
+                L.ops[nops + n] = (t.aS & kLitF) ? kLitF | (k.zb + ((t.aS & ~kLitF) - I)) : t.aS;
+                n++;
+                outp += t.aL;
+            }
+            if (t.bL) {
+                L.opp[nops + n] = outp;
+                L.ops[nops + n] = kLitF | (k.zb + ((t.bS & ~kLitF) - I));
+                n++;
+                outp += t.bL;
+            }
+            pos = t.pos;
+            st = t.st;
+        }
+    }
+    __syncthreads();
+
+    PieceOut r;
+    if (L.ctl[C_CUTLANE] != kNone) {
+        r.result = PR_FULL;
+        r.I = L.ctl[C_CUTPOS];
+        r.st = L.ctl[C_CUTST];
+        r.nops = nops + L.ctl[C_CUTOPS];
+        r.E = E + L.ctl[C_CUTBYTES];
+    } else {
+        r.nops = nops + L.ctl[C_TOPS];
+        r.E = E + L.ctl[C_TBYTES];
+        if (stoplane != kNone) {
+            const uint32_t sk = L.ctl[C_SKIND];
+            r.I = L.ctl[C_SPOS];
+            r.st = L.ctl[C_SST];
+            r.result = (sk & TK_BAD) ? PR_REFUSE : (sk & TK_EOF) ? PR_EOF : PR_OK;
+            if (sk & TK_EOF)
+                r.I = blk.z;
+        } else {
+            const uint32_t x = L.ex[fin][kNPL - 1];
+            r.I = I + (x >> 2);
+            r.st = x & 3u;
+            r.result = PR_OK;
+        }
+    }
+    if (r.result == PR_OK && r.I == I)
+        r.result = PR_REFUSE;                    // an instruction longer than a piece
+    r.I = uni(r.I);
+    r.st = uni(r.st);
+    r.nops = uni(r.nops);
+    r.E = uni(r.E);
+    r.result = uni(r.result);
+    if (tid == 0)
+        L.opp[r.nops] = r.E;                     // sentinel
+    __syncthreads();
+    return r;
+}
+
+// ---- window -------------------------------------------------------------------
+// Output [S, Ew) with the thread grid anchored at A = S & ~15 (bytes of the grid
+// below S or at/after Ew are rewritten with their own ring bytes).  Returns
+// false on a lookbehind error.  *iS: index of the op covering S, updated to
+// the op covering Ew.
+__device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, uint32_t& iS,
+                           uint32_t nops, uint32_t& cur)
+{
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const uint32_t A = S & ~15u, B = A + kW - 1, T = B - S;
+    const uint32_t tabb = A + kW;               // tab[i] at ring[(tabb + 2i) & 0xFFFF]
+    uint32_t* const bm = L.bmap[cur];
+
+    // op starts in (S, A + W) -> bitmap
+    for (uint32_t i = iS + 1 + tid; i < nops; i += kNT) {
+        const uint32_t p = L.opp[i];
+        if (p >= A + kW)
+            break;
+        atomicOr(&bm[(p - A) >> 5], 1u << ((p - A) & 31u));
+    }
+    __syncthreads();
+
+    const uint32_t o = wave * 512 + lane * 8;    // this thread's 8 bytes: A + o ..
+    const uint32_t x0 = A + o;
+    // ops before the wave's sub-window and in the whole window
+    const uint32_t d0 = bm[lane], d1 = bm[lane + 64];
+    const uint32_t pc0 = __builtin_popcount(d0), pc1 = __builtin_popcount(d1);
+    const uint32_t before = wave_sum((lane < 16 * wave ? pc0 : 0u) + (lane + 64 < 16 * wave ? pc1 : 0u));
+    const uint32_t total = wave_sum(pc0 + pc1);
+    const uint32_t bits8 = (bm[o >> 5] >> (o & 31u)) & 0xFFu;
+    const uint32_t lc = __builtin_popcount(bits8);
+    const uint32_t excl = wave_incl_scan(lc) - lc;
+    const uint32_t obase = iS + before + excl;
+
+    // source pointers
+    uint32_t e[8];
+    bool bad = false;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t x = x0 + i;
+        const uint32_t oi = obase + __builtin_popcount(bits8 & ((2u << i) - 1u));
+        uint32_t v = B - x;
+        if (x >= S && x < Ew) {
+            const uint32_t p = L.opp[oi], src = L.ops[oi];
+            if (src & kLitF) {
+                v = kLitBase + (src & 0xFFFFu) + (x - p);
+            } else {
+                const uint32_t d = src;
+                bad |= d > p;                    // lookbehind (lib/minilzo.c:3628)
+                const uint32_t q0 = p > S ? p : S;
+                const uint32_t kk = x - q0;      // < kW + 16
+                uint32_t qq = (uint32_t)((float)kk * __builtin_amdgcn_rcpf((float)d));
+                int32_t rr = (int32_t)(kk - qq * d);
+                rr += rr < 0 ? (int32_t)d : 0;
+                rr -= rr >= (int32_t)d ? (int32_t)d : 0;
+                const uint32_t t = q0 - d + (uint32_t)rr;
+                bad |= t >= x;                   // (never: keeps every chain strictly backward)
+                v = B - t;
+            }
+        }
+        e[i] = v;
+    }
+    if (bad)
+        L.ctl[C_REFUSE] = 1;
+    // pointer table slice (8 x u16 = 16 B, 16-aligned)
+    uint16_t* const ring16 = (uint16_t*)L.ring;
+    {
+        uint4 w;
+        w.x = e[0] | (e[1] << 16);
+        w.y = e[2] | (e[3] << 16);
+        w.z = e[4] | (e[5] << 16);
+        w.w = e[6] | (e[7] << 16);
+        *(uint4*)&L.ring[(tabb + 2 * o) & 0xFFFFu] = w;
+    }
+    // clear the other bitmap for the next window
+    if (tid < kW / 32)
+        L.bmap[cur ^ 1u][tid] = 0;
+    __syncthreads();
+    if (L.ctl[C_REFUSE])
+        return false;
+
+    // chase in-window sources (pointer table shared, written back as we go)
+    {
+        bool any = true;
+        volatile uint16_t* const vt = (volatile uint16_t*)ring16;
+        while (__ballot(any) != 0ull) {
+            any = false;
+#pragma unroll
+            for (uint32_t i = 0; i < 8; i++) {
+                const uint32_t x = x0 + i;
+                if (x >= S && x < Ew && e[i] <= T) {
+                    e[i] = vt[((tabb + 2 * (kW - 1 - e[i])) & 0xFFFFu) >> 1];
+                    any |= e[i] <= T;
+                }
+            }
+            volatile uint32_t* const vw = (volatile uint32_t*)&L.ring[(tabb + 2 * o) & 0xFFFFu];
+            vw[0] = e[0] | (e[1] << 16);
+            vw[1] = e[2] | (e[3] << 16);
+            vw[2] = e[4] | (e[5] << 16);
+            vw[3] = e[6] | (e[7] << 16);
+        }
+    }
+    __syncthreads();
+
+    // gather
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t x = x0 + i;
+        const bool valid = x >= S && x < Ew;
+        uint32_t v;
+        if (valid && e[i] >= kLitBase)
+            v = zbyte(L, e[i] - kLitBase);
+        else
+            v = L.ring[(valid ? B - e[i] : x) & 0xFFFFu];
+        if (i < 4)
+            lo |= v << (8 * i);
+        else
+            hi |= v << (8 * (i - 4));
+    }
+    // (no barrier: the ring bytes written here are never a final source)
+    *(uint2*)&L.ring[x0 & 0xFFFFu] = make_uint2(lo, hi);
+    if (x0 >= S && x0 + 8 <= Ew) {
+        *(uint2*)(blk.out + x0) = make_uint2(lo, hi);
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) {
+            const uint32_t x = x0 + i;
+            if (x >= S && x < Ew)
+                blk.out[x] = (uint8_t)((i < 4 ? lo >> (8 * i) : hi >> (8 * (i - 4))) & 0xFFu);
+        }
+    }
+    // op covering Ew
+    uint32_t nx = iS + total;
+    if (nx + 1 < nops && L.opp[nx + 1] <= Ew)
+        nx++;
+    iS = uni(nx);
+    cur ^= 1u;
+    __syncthreads();
+    return true;
+}
+
+__device__ void close_block(uint32_t b, bool ok, uint32_t len, uint32_t* out_len, int32_t* status,
+                            uint32_t* fallback, uint32_t* fallback_ids)
+{
+    if (threadIdx.x != 0)
+        return;
+    if (ok) {
+        out_len[b] = len;
+        status[b] = 0;
+    } else {
+        out_len[b] = 0xFA110000u;
+        status[b] = kFallback;
+        const uint32_t at = atomicAdd(&fallback[0], 1u);
+        fallback_ids[at] = b;
+    }
+}
+
+__global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
+    uint32_t* __restrict__ fallback, uint32_t* __restrict__ fallback_ids, uint32_t nblocks)
+{
+    __shared__ WinLds L;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks)
+        return;
+    const uint32_t tid = threadIdx.x;
+    Blk blk;
+    blk.in = src + src_off[b];
+    blk.z = src_len[b];
+    blk.out = dst + dst_off[b];
+    blk.cap = dst_cap[b];
+    // the exact decoder takes: empty or huge inputs, destinations not 8-aligned
+    if (blk.z == 0 || blk.z >= (1u << 24) || ((uintptr_t)blk.out & 7u)) {
+        close_block(b, false, 0, out_len, status, fallback, fallback_ids);
+        return;
+    }
+    if (tid < kW / 32) {
+        L.bmap[0][tid] = 0;
+        L.bmap[1][tid] = 0;
+    }
+    if (tid == 0)
+        L.ctl[C_REFUSE] = 0;
+    __syncthreads();
+
+    uint32_t I = 0, st = ST_F, E = 0, S = 0, iS = 0, nops = 0, cur = 0;
+    bool ok = true;
+    for (uint32_t k = 0;; k++) {
+        // carry the ops that still cover [S, E) to the front of the table
+        if (k) {
+            const uint32_t keep = nops - iS;      // ops iS .. nops-1, plus the sentinel
+            uint32_t v0 = 0, s0 = 0, v1 = 0, s1 = 0;
+            if (tid <= keep) {
+                v0 = L.opp[iS + tid];
+                s0 = tid < keep ? L.ops[iS + tid] : 0u;
+            }
+            if (tid + kNT <= keep) {
+                v1 = L.opp[iS + tid + kNT];
+                s1 = tid + kNT < keep ? L.ops[iS + tid + kNT] : 0u;
+            }
+            __syncthreads();
+            if (tid <= keep) {
+                L.opp[tid] = v0;
+                L.ops[tid] = s0;
+            }
+            if (tid + kNT <= keep) {
+                L.opp[tid + kNT] = v1;
+                L.ops[tid + kNT] = s1;
+            }
+            nops = keep;
+            iS = 0;
+        }
+        const uint32_t Pk = E;
+        const PieceOut r = parse_piece(L, blk, I, st, nops, E, k & 1u);
+        if (r.result == PR_REFUSE || r.E > blk.cap) {
+            ok = false;
+            break;
+        }
+        I = r.I;
+        st = r.st;
+        nops = r.nops;
+        E = r.E;
+        const bool eof = r.result == PR_EOF;
+        while (S < E && ((S & ~15u) + kW <= E || eof)) {
+            const uint32_t Ew = (S & ~15u) + kW < E ? (S & ~15u) + kW : E;
+            if (!run_window(L, blk, S, Ew, iS, nops, cur)) {
+                ok = false;
+                break;
+            }
+            S = Ew;
+        }
+        if (!ok)
+            break;
+        if (eof)
+            break;
+        if (S < E && (S < Pk || r.result == PR_FULL)) {
+            if (!run_window(L, blk, S, E, iS, nops, cur)) {
+                ok = false;
+                break;
+            }
+            S = E;
+        }
+    }
+    close_block(b, ok, E, out_len, status, fallback, fallback_ids);
+}
+
+}  // namespace
+
+extern "C" int lzo_mi355x_launch_decompress_win(const uint8_t* src, const uint64_t* src_off,
+                                                const uint32_t* src_len, uint8_t* dst,
+                                                const uint64_t* dst_off, const uint32_t* dst_cap,
+                                                uint32_t* out_len, int32_t* status,
+                                                uint32_t* fallback, uint32_t* fallback_ids,
+                                                uint32_t nblocks, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_decode_win_kernel, dim3(nblocks), dim3(kNT), 0, stream, src, src_off,
+                       src_len, dst, dst_off, dst_cap, out_len, status, fallback, fallback_ids,
+                       nblocks);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

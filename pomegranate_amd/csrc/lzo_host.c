@@ -236,7 +236,20 @@ size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
     return scr_ops_off(nblocks) + scr_sets(nblocks) * lzo_mi355x_fast_ops_bytes_per_block();
 }
 
-/* Fast decoder over the whole batch, then the exact decoder over the blocks
+/* Which throughput decoder runs: the windowed one (lzo1x_decode_win.hip,
+ * default) or the round-2 op-set decoder (lzo1x_decode_fast.hip) with
+ * POM_DECODER=fast, kept for A/B measurements. */
+static int use_win_decoder(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("POM_DECODER");
+        v = !(e && strcmp(e, "fast") == 0);
+    }
+    return v;
+}
+
+/* Throughput decoder over the whole batch, then the exact decoder over the blocks
  * it refused (malformed input, capacity/lookbehind errors, pathological
  * streams).  Without scratch every block takes the exact decoder.
  * unchecked: the exact decoder follows the unchecked lzo1x_decompress (the
@@ -255,13 +268,22 @@ static int decompress_dev(const uint8_t *src, const uint64_t *src_off, const uin
     uint8_t *scr = scratch;
     const uint32_t nsets = (uint32_t)scr_sets(nblocks);
     uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nblocks));
-    if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)
-        return -1;
-    if (lzo_mi355x_launch_decompress_fast(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                          status, fb, ids, (uint32_t *)(scr + SCR_POOL),
-                                          scr + SCR_RING,
-                                          scr + scr_ops_off(nblocks), nsets, nblocks, s) != 0)
-        return -1;
+    if (use_win_decoder()) {
+        /* the windowed decoder: no op sets, only the fallback list */
+        if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
+            return -1;
+        if (lzo_mi355x_launch_decompress_win(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
+                                             status, fb, ids, nblocks, s) != 0)
+            return -1;
+    } else {
+        if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)
+            return -1;
+        if (lzo_mi355x_launch_decompress_fast(src, src_off, src_len, dst, dst_off, dst_cap,
+                                              out_len, status, fb, ids,
+                                              (uint32_t *)(scr + SCR_POOL), scr + SCR_RING,
+                                              scr + scr_ops_off(nblocks), nsets, nblocks, s) != 0)
+            return -1;
+    }
     const uint32_t ngrid = nblocks < 512 ? nblocks : 512;
     return lzo_mi355x_launch_decompress_exact(src, src_off, src_len, dst, dst_off, dst_cap,
                                               out_len, status, fb, ids, ngrid, nblocks, unchecked,

@@ -71,6 +71,16 @@ int lzo_mi355x_launch_decompress_fast(const uint8_t *src, const uint64_t *src_of
                                       void *ops, uint32_t nsets, uint32_t nblocks,
                                       hipStream_t stream);
 
+/* Windowed throughput decoder (lzo1x_decode_win.hip): one workgroup of 512
+ * threads per block, 64 KiB LDS output ring.  Blocks it does not finish
+ * exactly go to fallback_ids[] as with the fast decoder (*fallback = 0 on
+ * entry). */
+int lzo_mi355x_launch_decompress_win(const uint8_t *src, const uint64_t *src_off,
+                                     const uint32_t *src_len, uint8_t *dst,
+                                     const uint64_t *dst_off, const uint32_t *dst_cap,
+                                     uint32_t *out_len, int32_t *status, uint32_t *fallback,
+                                     uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
+
 /* Unchecked-decoder pre-scan: decoded length and status per block; with
  * cap_out, also min(length, cap_limit) per block (a decode's capacity). */
 int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off,
