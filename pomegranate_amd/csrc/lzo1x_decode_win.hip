@@ -20,8 +20,8 @@
 //        to an LDS op table of kOpCap entries;
 //  * WINDOWS of output (kW = 4 KiB, lane = 8 output bytes): every output byte
 //    gets a source pointer, encoded as e = B - t for a source at output
-//    position t (B = window end - 1) or kLitBase + zin offset for a literal
-//    byte.  Matches that overlap themselves (distance d < length) are reduced
+//    position t (B = window end - 1); literal bytes are written into the ring
+//    first and point at themselves as final (e = kFin + offset).  Matches that overlap themselves (distance d < length) are reduced
 //    to the last period before max(op start, window start).  A source inside
 //    the window (e <= T) is followed through the window's pointer table
 //    (e = tab[W - 1 - e], with write-back, so chains shorten as they are
@@ -53,16 +53,17 @@ constexpr uint32_t kOpCap = 1024;                // ops held at once
 constexpr uint32_t kG = 16;                      // parse segment bytes
 constexpr uint32_t kNPL = kZH / kG;              // parse lanes (waves 0-1)
 constexpr uint32_t kLook = 16;                   // speculative lead-in
-constexpr uint32_t kLitBase = 65536u - kZR;      // e >= kLitBase: literal at zin[e - kLitBase]
-constexpr uint32_t kLitF = 0x80000000u;
+constexpr uint32_t kFin = 53248u;                // e >= kFin: final byte at ring[A + e - kFin]
+constexpr uint32_t kLitF = 0x80000000u;          // op source: literal ...
+constexpr uint32_t kLitG = 0x40000000u;          // ... at an input position (else a zin offset)
 constexpr int32_t kFallback = 0x7FFF0001;
 static_assert(kW * 8 == kNT * 64, "window: 8 bytes per thread");
 static_assert(2 * kW <= 65536u - 0xBFFFu - 1u, "pointer table slots must be dead ring slots");
-static_assert(0xBFFFu + kW < kLitBase, "e encoding: match pointers below literal ones");
+static_assert(0xBFFFu + kW < kFin && kFin + kW <= 65536u, "e encoding: match pointers below final ones");
 static_assert(kNPL == 2 * kWave, "two parse waves");
 
 enum : uint32_t { ST_A = 0, ST_B = 1, ST_C = 2, ST_F = 3 };
-enum : uint32_t { TK_EOF = 1, TK_BAD = 2, TK_CUT = 4 };
+enum : uint32_t { TK_EOF = 1, TK_BAD = 2 };
 // piece results
 enum : uint32_t { PR_OK = 0, PR_EOF = 1, PR_FULL = 2, PR_REFUSE = 3 };
 // control words
@@ -108,14 +109,20 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return __builtin_amdg
 struct Piece {
     uint32_t I;          // input position of zin byte zb
     uint32_t zb;         // byte offset of the piece's half in zin
-    uint32_t lim;        // min(z, I + kZH): bytes below are real staged input
+    uint32_t sEnd;       // I + kZH: [I, sEnd) is staged (zero past z)
     uint32_t z;
-    bool lim_is_z;       // the piece holds the end of the input
+    const uint8_t* in;   // the whole compressed block (HBM)
 };
 
 __device__ __forceinline__ uint32_t zbyte(const WinLds& L, uint32_t off)
 {
     return (L.zin[off >> 2] >> (8u * (off & 3u))) & 0xFFu;
+}
+
+// input byte p < z: from the staged piece, or from HBM past it
+__device__ __forceinline__ uint32_t in_byte(const WinLds& L, const Piece& k, uint32_t p)
+{
+    return p < k.sEnd ? zbyte(L, k.zb + (p - k.I)) : (uint32_t)k.in[p];
 }
 
 struct Tok {
@@ -125,9 +132,9 @@ struct Tok {
     uint32_t fl;         // TK_*
 };
 
-// One instruction at (pos, st), pos < k.lim, general form (long length
-// extensions).  Bytes at or past k.lim read as 0; the caller's flag logic
-// (tok_flags) classifies the instruction by where it ends.
+// One instruction at (pos, st), general form: long length extensions and
+// instructions that run past the staged piece (bytes read from HBM).  Bytes
+// at or past z read as 0 and make the instruction TK_BAD.
 __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t pos, uint32_t st)
 {
     Tok r;
@@ -136,11 +143,11 @@ __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t po
     uint32_t far = 0;    // furthest byte read + 1
     auto rd = [&](uint32_t p) -> uint32_t {
         far = p + 1 > far ? p + 1 : far;
-        return p < k.lim ? zbyte(L, k.zb + (p - k.I)) : 0u;
+        return p < k.z ? in_byte(L, k, p) : 0u;
     };
     auto ext = [&](uint32_t& p, uint32_t base) -> uint32_t {
         uint32_t v = 0;
-        while (p < k.lim && rd(p) == 0) {
+        while (p < k.z && rd(p) == 0) {
             v += 255;
             p++;
         }
@@ -170,8 +177,6 @@ __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t po
             r.aS = kLitF | pos;
             r.pos = pos + t + 3;
             r.st = ST_B;
-            if (r.pos < pos)
-                r.pos = 0xFFFFFFF0u;             // wrapped: ends past anything
             goto done;
         }
         if (t < 16) {
@@ -220,11 +225,10 @@ __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t po
         r.pos = pos;
     }
 done:
-    // classify by the furthest byte the instruction needs
     {
         const uint32_t need = far > r.pos ? far : r.pos;
-        if (need > k.lim)
-            r.fl = k.lim_is_z ? TK_BAD : TK_CUT;
+        if (need > k.z || r.pos < pos)
+            r.fl = TK_BAD;                       // runs past the input (INPUT_OVERRUN)
         else if ((r.fl & TK_EOF) && r.pos != k.z)
             r.fl = TK_BAD;                       // EOF not at the end (INPUT_NOT_CONSUMED)
     }
@@ -232,7 +236,8 @@ done:
 }
 
 // Branch-free form for the common case: the instruction's fields lie in its
-// first 4 bytes (no 255-chunk length extension).  One zin round trip.
+// first 4 bytes (no 255-chunk length extension) inside the staged piece.
+// One zin round trip.
 __device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos, uint32_t st)
 {
     const uint32_t off = k.zb + (pos - k.I);
@@ -246,7 +251,7 @@ __device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos
     const bool m3 = !flit && t >= 32 && t < 64;
     const bool m4 = !flit && t >= 16 && t < 32;
     const bool ext = (lit && t == 0) || (m3 && (t & 31) == 0) || (m4 && (t & 7) == 0);
-    if (__builtin_expect(ext && b1 == 0, 0))
+    if (__builtin_expect((ext && b1 == 0) || pos + 4 > k.sEnd, 0))
         return tok_slow(L, k, pos, st);
     const uint32_t e = ext ? 1u : 0u;
     const uint32_t o16 = __builtin_amdgcn_ubfe(lo, 8u + 8u * e, 16);
@@ -272,12 +277,7 @@ __device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos
     r.pos = islit ? pos + hdr + nlit : pos + used + (eof ? 0u : tl);
     r.st = islit ? (flit && nlit < 4 ? ST_C : ST_B) : (tl && !eof ? ST_C : ST_A);
     // the instruction (header, then literals) ends at r.pos
-    uint32_t fl = eof ? TK_EOF : 0u;
-    if (r.pos > k.lim)
-        fl = k.lim_is_z ? TK_BAD : TK_CUT;
-    else if (eof && r.pos != k.z)
-        fl = TK_BAD;
-    r.fl = fl;
+    r.fl = r.pos > k.z ? TK_BAD : eof ? (r.pos != k.z ? TK_BAD : TK_EOF) : 0u;
     return r;
 }
 
@@ -305,8 +305,8 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
     k.I = I;
     k.zb = half * kZH;
     k.z = blk.z;
-    k.lim = blk.z < I + kZH ? blk.z : I + kZH;
-    k.lim_is_z = blk.z <= I + kZH;
+    k.sEnd = I + kZH;
+    k.in = blk.in;
 
     // stage: thread t loads input bytes I + 4t .. +3 (0 past z)
     {
@@ -336,7 +336,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
 
     // P1: speculative walks
     if (pl) {
-        if (a >= k.lim && j) {
+        if (a >= blk.z && j) {
             sx = pack_pt(k, b, ST_A);
         } else {
             uint32_t pos = j ? (a >= I + kLook ? a - kLook : I) : I;
@@ -345,7 +345,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
             while (pos < b) {
                 const Tok t = tok(L, k, pos, st);
                 if (t.fl) {
-                    if (j == 0 || (t.fl & (TK_CUT | TK_EOF)))
+                    if (j == 0 || (t.fl & TK_EOF))
                         break;                   // stop point
                     restart++;                   // impossible guess: start one byte later
                     pos = restart;
@@ -402,32 +402,45 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
         }
     };
 
-    // P2: exits from true entries (Jacobi over the lanes, double-buffered)
+    // P2: exits from true entries.  Inside each parse wave the exits settle by
+    // Jacobi steps over the lanes (entry = the lane below's exit, by shuffle;
+    // a lane re-walks only when its entry changed), no barrier; then wave 1
+    // settles again once wave 0's last exit is known.
+    const uint32_t lane = lane_id();
     uint32_t my_ent = kNone, my_ex = sx;
-    uint32_t it = 0;
-    for (;; it++) {
-        const uint32_t cur = it & 1u;
-        __syncthreads();
-        if (pl && j) {
-            const uint32_t ent = L.ex[cur][j - 1];
-            if (ent != my_ent) {
-                my_ent = ent;
-                const uint32_t nx = exit_from(ent);
-                if (nx != my_ex) {
-                    my_ex = nx;
-                    atomicAdd(&L.cnt[it % 3], 1u);
-                }
+    auto settle = [&](uint32_t lane0_entry) {
+        for (;;) {
+            uint32_t e = (uint32_t)__shfl_up((int)my_ex, 1, kWave);
+            if (lane == 0)
+                e = lane0_entry;
+            bool ch = false;
+            if (e != my_ent) {
+                my_ent = e;
+                const uint32_t nx = exit_from(e);
+                ch = nx != my_ex;
+                my_ex = nx;
             }
+            if (__ballot(ch) == 0ull)
+                break;
         }
-        if (pl)
-            L.ex[cur ^ 1u][j] = my_ex;
-        if (tid == 0)
-            L.cnt[(it + 1) % 3] = 0;
-        __syncthreads();
-        if (L.cnt[it % 3] == 0)
-            break;
+    };
+    __syncthreads();                             // spec exits in ex[0]
+    uint32_t w1_entry = 0;
+    if (pl) {
+        w1_entry = L.ex[0][kWave - 1];           // wave 1 starts from wave 0's spec exit
+        settle(tid < kWave ? entry0 : w1_entry);
+        L.ex[1][j] = my_ex;
     }
-    const uint32_t fin = (it + 1) & 1u;          // ex[fin] holds the settled exits
+    __syncthreads();
+    if (pl && tid >= kWave) {
+        const uint32_t e63 = L.ex[1][kWave - 1];
+        if (e63 != w1_entry) {                   // wave-uniform
+            settle(e63);
+            L.ex[1][j] = my_ex;
+        }
+    }
+    __syncthreads();
+    const uint32_t fin = 1;                      // ex[1] holds the settled exits
     const uint32_t ent = pl ? (j ? L.ex[fin][j - 1] : entry0) : 0u;
 
     // P3: count ops and bytes on the true path
@@ -452,6 +465,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
     }
     // scan over the two parse waves
     const uint32_t wave = tid >> 6;
+    (void)lane;
     const uint32_t i_ops = wave_incl_scan(c_ops), i_bytes = wave_incl_scan(c_bytes);
     if (tid == 63) {
         L.wsum[0] = i_ops;
@@ -471,6 +485,11 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
         L.ctl[C_TBYTES] = b_bytes + c_bytes;
     }
 
+    // literal source: a zin offset when the bytes are staged, else the input
+    // position (long literal runs past the piece are read from HBM)
+    auto lit_src = [&](uint32_t q, uint32_t n) -> uint32_t {
+        return q + n <= k.sEnd ? kLitF | (k.zb + (q - I)) : kLitF | kLitG | q;
+    };
     // P4: emit ops (stop at the op cap: that instruction starts the next piece)
     const uint32_t avail = kOpCap - nops;
     if (pl && c_ops && b_ops <= avail) {
@@ -491,13 +510,13 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
             }
             if (t.aL) {
                 L.opp[nops + n] = outp;
-                L.ops[nops + n] = (t.aS & kLitF) ? kLitF | (k.zb + ((t.aS & ~kLitF) - I)) : t.aS;
+                L.ops[nops + n] = (t.aS & kLitF) ? lit_src(t.aS & ~kLitF, t.aL) : t.aS;
                 n++;
                 outp += t.aL;
             }
             if (t.bL) {
                 L.opp[nops + n] = outp;
-                L.ops[nops + n] = kLitF | (k.zb + ((t.bS & ~kLitF) - I));
+                L.ops[nops + n] = lit_src(t.bS & ~kLitF, t.bL);
                 n++;
                 outp += t.bL;
             }
@@ -578,8 +597,9 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
     const uint32_t excl = wave_incl_scan(lc) - lc;
     const uint32_t obase = iS + before + excl;
 
-    // source pointers
+    // source pointers; literal bytes go straight into the ring (final)
     uint32_t e[8];
+    uint32_t lmask = 0, lv0 = 0, lv1 = 0;
     bool bad = false;
 #pragma unroll
     for (uint32_t i = 0; i < 8; i++) {
@@ -589,7 +609,14 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
         if (x >= S && x < Ew) {
             const uint32_t p = L.opp[oi], src = L.ops[oi];
             if (src & kLitF) {
-                v = kLitBase + (src & 0xFFFFu) + (x - p);
+                const uint32_t c = (src & kLitG) ? (uint32_t)blk.in[(src & 0xFFFFFFu) + (x - p)]
+                                                 : zbyte(L, (src & 0xFFFFu) + (x - p));
+                lmask |= 1u << i;
+                if (i < 4)
+                    lv0 |= c << (8 * i);
+                else
+                    lv1 |= c << (8 * (i - 4));
+                v = kFin + (x - A);
             } else {
                 const uint32_t d = src;
                 bad |= d > p;                    // lookbehind (lib/minilzo.c:3628)
@@ -617,6 +644,19 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
         w.z = e[4] | (e[5] << 16);
         w.w = e[6] | (e[7] << 16);
         *(uint4*)&L.ring[(tabb + 2 * o) & 0xFFFFu] = w;
+    }
+    if (lmask) {
+        uint2* const slot = (uint2*)&L.ring[x0 & 0xFFFFu];
+        uint2 w = *slot;
+        uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            m0 |= (lmask >> i) & 1u ? 0xFFu << (8 * i) : 0u;
+            m1 |= (lmask >> (i + 4)) & 1u ? 0xFFu << (8 * i) : 0u;
+        }
+        w.x = (w.x & ~m0) | (lv0 & m0);
+        w.y = (w.y & ~m1) | (lv1 & m1);
+        *slot = w;
     }
     // clear the other bitmap for the next window
     if (tid < kW / 32)
@@ -654,11 +694,8 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
     for (uint32_t i = 0; i < 8; i++) {
         const uint32_t x = x0 + i;
         const bool valid = x >= S && x < Ew;
-        uint32_t v;
-        if (valid && e[i] >= kLitBase)
-            v = zbyte(L, e[i] - kLitBase);
-        else
-            v = L.ring[(valid ? B - e[i] : x) & 0xFFFFu];
+        const uint32_t y = !valid ? x : e[i] >= kFin ? A + (e[i] - kFin) : B - e[i];
+        const uint32_t v = L.ring[y & 0xFFFFu];
         if (i < 4)
             lo |= v << (8 * i);
         else
