@@ -83,6 +83,7 @@ struct __attribute__((aligned(16))) WinLds {
     uint32_t wsum[4];
     uint32_t cnt[4];
     uint32_t ctl[C_N];
+    uint64_t stamp[16];                          // diagnostics (STAMPS builds)
 };
 static_assert(sizeof(WinLds) <= 81920, "two workgroups per CU");
 
@@ -283,6 +284,22 @@ __device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos
 
 __device__ __forceinline__ uint32_t pack_pt(const Piece& k, uint32_t pos, uint32_t st) { return ((pos - k.I) << 2) | st; }
 
+// ---- diagnostics: per-phase cycle stamps (STAMPS builds only) ----------------
+// (thread 0 accumulates into L.stamp; L.stamp[15] holds the last time)
+#define STAMP(i)                                                   \
+    do {                                                           \
+        if (STAMPS && threadIdx.x == 0) {                          \
+            const uint64_t _t = clock64();                         \
+            L.stamp[(i)] += _t - L.stamp[15];                      \
+            L.stamp[15] = _t;                                      \
+        }                                                          \
+    } while (0)
+#define COUNT(i, n)                                                \
+    do {                                                           \
+        if (STAMPS && threadIdx.x == 0)                            \
+            L.stamp[(i)] += (n);                                   \
+    } while (0)
+
 // ---- block state ----------------------------------------------------------
 struct Blk {
     const uint8_t* in;
@@ -297,8 +314,9 @@ struct PieceOut {
     uint32_t nops, E;    // op count and output end after the piece
 };
 
-__device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t st_in, uint32_t nops,
-                                uint32_t E, uint32_t half)
+template <bool STAMPS>
+__device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t st_in,
+                                                uint32_t nops, uint32_t E, uint32_t half)
 {
     const uint32_t tid = threadIdx.x;
     Piece k;
@@ -327,6 +345,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
             L.cnt[tid] = 0;
     }
     __syncthreads();
+    STAMP(0);
 
     const bool pl = tid < kNPL;
     const uint32_t j = tid;
@@ -420,11 +439,13 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
                 ch = nx != my_ex;
                 my_ex = nx;
             }
+            COUNT(12, 1);
             if (__ballot(ch) == 0ull)
                 break;
         }
     };
     __syncthreads();                             // spec exits in ex[0]
+    STAMP(1);
     uint32_t w1_entry = 0;
     if (pl) {
         w1_entry = L.ex[0][kWave - 1];           // wave 1 starts from wave 0's spec exit
@@ -440,6 +461,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
         }
     }
     __syncthreads();
+    STAMP(2);
     const uint32_t fin = 1;                      // ex[1] holds the settled exits
     const uint32_t ent = pl ? (j ? L.ex[fin][j - 1] : entry0) : 0u;
 
@@ -472,6 +494,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
         L.wsum[1] = i_bytes;
     }
     __syncthreads();
+    STAMP(3);
     const uint32_t b_ops = i_ops - c_ops + (wave == 1 ? L.wsum[0] : 0u);
     const uint32_t b_bytes = i_bytes - c_bytes + (wave == 1 ? L.wsum[1] : 0u);
     const uint32_t stoplane = L.ctl[C_STOPLANE];
@@ -525,6 +548,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
         }
     }
     __syncthreads();
+    STAMP(4);
 
     PieceOut r;
     if (L.ctl[C_CUTLANE] != kNone) {
@@ -559,7 +583,9 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
     r.result = uni(r.result);
     if (tid == 0)
         L.opp[r.nops] = r.E;                     // sentinel
+    COUNT(10, 1);
     __syncthreads();
+    STAMP(4);
     return r;
 }
 
@@ -568,8 +594,9 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
 // below S or at/after Ew are rewritten with their own ring bytes).  Returns
 // false on a lookbehind error.  *iS: index of the op covering S, updated to
 // the op covering Ew.
+template <bool STAMPS>
 __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, uint32_t& iS,
-                           uint32_t nops, uint32_t& cur)
+                                           uint32_t nops, uint32_t& cur)
 {
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const uint32_t A = S & ~15u, B = A + kW - 1, T = B - S;
@@ -584,6 +611,7 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
         atomicOr(&bm[(p - A) >> 5], 1u << ((p - A) & 31u));
     }
     __syncthreads();
+    STAMP(5);
 
     const uint32_t o = wave * 512 + lane * 8;    // this thread's 8 bytes: A + o ..
     const uint32_t x0 = A + o;
@@ -662,6 +690,7 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
     if (tid < kW / 32)
         L.bmap[cur ^ 1u][tid] = 0;
     __syncthreads();
+    STAMP(6);
     if (L.ctl[C_REFUSE])
         return false;
 
@@ -679,6 +708,7 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
                     any |= e[i] <= T;
                 }
             }
+            COUNT(11, 1);
             volatile uint32_t* const vw = (volatile uint32_t*)&L.ring[(tabb + 2 * o) & 0xFFFFu];
             vw[0] = e[0] | (e[1] << 16);
             vw[1] = e[2] | (e[3] << 16);
@@ -687,6 +717,7 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
         }
     }
     __syncthreads();
+    STAMP(7);
 
     // gather
     uint32_t lo = 0, hi = 0;
@@ -719,7 +750,9 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
         nx++;
     iS = uni(nx);
     cur ^= 1u;
+    COUNT(9, 1);
     __syncthreads();
+    STAMP(8);
     return true;
 }
 
@@ -739,14 +772,18 @@ __device__ void close_block(uint32_t b, bool ok, uint32_t len, uint32_t* out_len
     }
 }
 
+template <bool STAMPS>
 __global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
-    uint32_t* __restrict__ fallback, uint32_t* __restrict__ fallback_ids, uint32_t nblocks)
+    uint32_t* __restrict__ fallback, uint32_t* __restrict__ fallback_ids, uint32_t nblocks,
+    uint64_t* __restrict__ dbg)
 {
     __shared__ WinLds L;
+    if (STAMPS && threadIdx.x < 16)
+        L.stamp[threadIdx.x] = threadIdx.x == 15 ? clock64() : 0;
     const uint32_t b = blockIdx.x;
     if (b >= nblocks)
         return;
@@ -797,7 +834,7 @@ __global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
             iS = 0;
         }
         const uint32_t Pk = E;
-        const PieceOut r = parse_piece(L, blk, I, st, nops, E, k & 1u);
+        const PieceOut r = parse_piece<STAMPS>(L, blk, I, st, nops, E, k & 1u);
         if (r.result == PR_REFUSE || r.E > blk.cap) {
             ok = false;
             break;
@@ -809,7 +846,7 @@ __global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
         const bool eof = r.result == PR_EOF;
         while (S < E && ((S & ~15u) + kW <= E || eof)) {
             const uint32_t Ew = (S & ~15u) + kW < E ? (S & ~15u) + kW : E;
-            if (!run_window(L, blk, S, Ew, iS, nops, cur)) {
+            if (!run_window<STAMPS>(L, blk, S, Ew, iS, nops, cur)) {
                 ok = false;
                 break;
             }
@@ -820,7 +857,7 @@ __global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
         if (eof)
             break;
         if (S < E && (S < Pk || r.result == PR_FULL)) {
-            if (!run_window(L, blk, S, E, iS, nops, cur)) {
+            if (!run_window<STAMPS>(L, blk, S, E, iS, nops, cur)) {
                 ok = false;
                 break;
             }
@@ -828,6 +865,9 @@ __global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
         }
     }
     close_block(b, ok, E, out_len, status, fallback, fallback_ids);
+    if (STAMPS && tid == 0)
+        for (int i = 0; i < 16; i++)
+            dbg[(size_t)b * 16 + i] = L.stamp[i];
 }
 
 }  // namespace
@@ -841,8 +881,28 @@ extern "C" int lzo_mi355x_launch_decompress_win(const uint8_t* src, const uint64
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_decode_win_kernel, dim3(nblocks), dim3(kNT), 0, stream, src, src_off,
-                       src_len, dst, dst_off, dst_cap, out_len, status, fallback, fallback_ids,
-                       nblocks);
+    hipLaunchKernelGGL(lzo1x_decode_win_kernel<false>, dim3(nblocks), dim3(kNT), 0, stream, src,
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
+                       fallback_ids, nblocks, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Diagnostic: the same decoder with per-phase cycle stamps (16 x u64 per block,
+// thread 0's view): 0 stage, 1 speculative walks, 2 settle, 3 count + scan,
+// 4 emit, 5 window op bitmap, 6 pointers, 7 chase, 8 gather + stores;
+// counts: 9 windows, 10 pieces, 11 chase rounds (wave 0), 12 settle rounds (wave 0).
+extern "C" int lzo_mi355x_debug_decompress_win_stamps(const uint8_t* src, const uint64_t* src_off,
+                                                      const uint32_t* src_len, uint8_t* dst,
+                                                      const uint64_t* dst_off, const uint32_t* dst_cap,
+                                                      uint32_t* out_len, int32_t* status,
+                                                      uint32_t* fallback, uint32_t* fallback_ids,
+                                                      uint32_t nblocks, uint64_t* stamps,
+                                                      hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_decode_win_kernel<true>, dim3(nblocks), dim3(kNT), 0, stream, src,
+                       src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
+                       fallback_ids, nblocks, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

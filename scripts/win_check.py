@@ -59,15 +59,14 @@ if not a.skip_exact:
             lzo.decompress_dev(zsrc, ob, ol, st, scr)
             torch.cuda.synchronize()
             fb = int(scr[:4].view(torch.int32).item())
-            ok = torch.equal(out, src.arena) and bool((st == 0).all()) and \
-                bool((ol.cpu().numpy() == lens.astype(np.int32)).all())
             bad = []
-            if not ok:
-                o = out.cpu().numpy(); s = src.arena.cpu().numpy()
-                offs = src.off.cpu().numpy()
-                for i, n in enumerate(lens):
-                    if not np.array_equal(o[offs[i]:offs[i] + n], s[offs[i]:offs[i] + n]) or int(st[i]) != 0:
-                        bad.append((i, int(n), int(st[i]), int(ol[i])))
+            o = out.cpu().numpy(); s = src.arena.cpu().numpy()
+            offs = src.off.cpu().numpy(); stn = st.cpu().numpy(); oln = ol.cpu().numpy()
+            for i, n in enumerate(lens):
+                if not np.array_equal(o[offs[i]:offs[i] + n], s[offs[i]:offs[i] + n]) or \
+                        int(stn[i]) != 0 or int(oln[i]) != int(n):
+                    bad.append((i, int(n), int(stn[i]), int(oln[i])))
+            ok = not bad
             results[f"{synth.MODEL_NAMES[model]}/{rnd}"] = {"ok": ok, "fallbacks": fb, "bad": bad[:5]}
             print(synth.MODEL_NAMES[model], rnd, ok, "fallbacks", fb, bad[:5], flush=True)
 
