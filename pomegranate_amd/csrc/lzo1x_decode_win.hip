@@ -47,12 +47,13 @@ namespace {
 constexpr uint32_t kWave = 64;
 constexpr uint32_t kNT = 512;                    // threads per workgroup (8 waves)
 constexpr uint32_t kW = 4096;                    // window bytes (8 per thread)
-constexpr uint32_t kZH = 2048;                   // compressed bytes per piece
-constexpr uint32_t kZR = 2 * kZH;                // zin ring (two pieces)
+constexpr uint32_t kZH = 2048;                   // compressed bytes per piece (instruction starts)
+constexpr uint32_t kZS = kZH + 64;               // bytes staged per piece (headers past its end)
+constexpr uint32_t kZR = 2 * kZS;                // zin ring (two pieces)
 constexpr uint32_t kOpCap = 1024;                // ops held at once
-constexpr uint32_t kG = 16;                      // parse segment bytes
-constexpr uint32_t kNPL = kZH / kG;              // parse lanes (waves 0-1)
-constexpr uint32_t kLook = 16;                   // speculative lead-in
+constexpr uint32_t kG = 32;                      // parse segment bytes
+constexpr uint32_t kNPL = kZH / kG;              // parse lanes (wave 0)
+constexpr uint32_t kLook = 32;                   // speculative lead-in
 constexpr uint32_t kFin = 53248u;                // e >= kFin: final byte at ring[A + e - kFin]
 constexpr uint32_t kLitF = 0x80000000u;          // op source: literal ...
 constexpr uint32_t kLitG = 0x40000000u;          // ... at an input position (else a zin offset)
@@ -60,18 +61,14 @@ constexpr int32_t kFallback = 0x7FFF0001;
 static_assert(kW * 8 == kNT * 64, "window: 8 bytes per thread");
 static_assert(2 * kW <= 65536u - 0xBFFFu - 1u, "pointer table slots must be dead ring slots");
 static_assert(0xBFFFu + kW < kFin && kFin + kW <= 65536u, "e encoding: match pointers below final ones");
-static_assert(kNPL == 2 * kWave, "two parse waves");
+static_assert(kNPL == kWave, "one parse wave");
 
 enum : uint32_t { ST_A = 0, ST_B = 1, ST_C = 2, ST_F = 3 };
 enum : uint32_t { TK_EOF = 1, TK_BAD = 2 };
 // piece results
 enum : uint32_t { PR_OK = 0, PR_EOF = 1, PR_FULL = 2, PR_REFUSE = 3 };
 // control words
-enum : uint32_t {
-    C_REFUSE = 0, C_STOPLANE, C_SPOS, C_SST, C_SKIND, C_CUTLANE, C_CUTPOS, C_CUTST, C_CUTOPS,
-    C_CUTBYTES, C_TOPS, C_TBYTES, C_N = 16
-};
-constexpr uint32_t kNone = 0xFFFFFFFFu;
+enum : uint32_t { C_REFUSE = 0, C_SPOS, C_SST, C_SKIND, C_TOPS, C_TBYTES, C_N = 16 };
 
 struct __attribute__((aligned(16))) WinLds {
     uint8_t ring[65536];
@@ -79,9 +76,6 @@ struct __attribute__((aligned(16))) WinLds {
     uint32_t opp[kOpCap + 4];                    // op output start; opp[nops] = end
     uint32_t ops[kOpCap];                        // kLitF | zin offset, or match distance
     uint32_t bmap[2][kW / 32];                   // op starts of the window
-    uint32_t ex[2][kNPL];                        // parse-lane exits (rel pos << 2 | state)
-    uint32_t wsum[4];
-    uint32_t cnt[4];
     uint32_t ctl[C_N];
     uint64_t stamp[16];                          // diagnostics (STAMPS builds)
 };
@@ -110,7 +104,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) { return __builtin_amdg
 struct Piece {
     uint32_t I;          // input position of zin byte zb
     uint32_t zb;         // byte offset of the piece's half in zin
-    uint32_t sEnd;       // I + kZH: [I, sEnd) is staged (zero past z)
+    uint32_t sEnd;       // I + kZS: [I, sEnd) is staged (zero past z)
     uint32_t z;
     const uint8_t* in;   // the whole compressed block (HBM)
 };
@@ -316,45 +310,46 @@ struct PieceOut {
 
 template <bool STAMPS>
 __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t st_in,
-                                                uint32_t nops, uint32_t E, uint32_t half)
+                                uint32_t nops, uint32_t E, uint32_t half)
 {
     const uint32_t tid = threadIdx.x;
     Piece k;
     k.I = I;
-    k.zb = half * kZH;
+    k.zb = half * kZS;
     k.z = blk.z;
-    k.sEnd = I + kZH;
+    k.sEnd = I + kZS;
     k.in = blk.in;
 
-    // stage: thread t loads input bytes I + 4t .. +3 (0 past z)
+    // stage kZS bytes from I (0 past z): thread t the dwords t and t + kNT
     {
-        const uint32_t p = I + 4 * tid;
-        uint32_t v = 0;
-        if (p + 4 <= blk.z) {
-            const uint8_t* q = blk.in + p;
-            v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-        } else {
-            for (uint32_t i = 0; i < 4; i++)
-                if (p + i < blk.z)
-                    v |= (uint32_t)blk.in[p + i] << (8 * i);
+        const uintptr_t base = (uintptr_t)(blk.in + I);
+        const uint32_t sh = (uint32_t)(base & 3u);
+        const uint32_t* aw = (const uint32_t*)(base - sh);
+        for (uint32_t w = tid; w < kZS / 4; w += kNT) {
+            const uint32_t p = I + 4 * w;
+            uint32_t v = 0;
+            if (p - sh + 8 <= blk.z) {            // both aligned dwords inside the input
+                v = __builtin_amdgcn_alignbyte(aw[w + 1], aw[w], sh);
+            } else {
+                for (uint32_t i = 0; i < 4; i++)
+                    if (p + i < blk.z)
+                        v |= (uint32_t)blk.in[p + i] << (8 * i);
+            }
+            L.zin[(k.zb >> 2) + w] = v;
         }
-        L.zin[(k.zb >> 2) + tid] = v;
-        if (tid < C_N)
-            L.ctl[tid] = tid == C_STOPLANE || tid == C_CUTLANE ? kNone : 0u;
-        if (tid < 4)
-            L.cnt[tid] = 0;
     }
     __syncthreads();
     STAMP(0);
 
-    const bool pl = tid < kNPL;
-    const uint32_t j = tid;
-    const uint32_t a = I + kG * j, b = a + kG;
-    const uint32_t entry0 = pack_pt(k, I, st_in);
-    uint32_t bm0 = 0, bm1 = 0, bm2 = 0, sx = 0;
+    PieceOut r;
+    if (tid < kWave) {
+        // ---- wave 0: the parse; lane j owns input segment [a, b) ------------
+        const uint32_t j = tid;
+        const uint32_t a = I + kG * j, b = a + kG;
+        const uint32_t entry0 = pack_pt(k, I, st_in);
+        uint32_t bm0 = 0, bm1 = 0, bm2 = 0, sx;
 
-    // P1: speculative walks
-    if (pl) {
+        // P1: speculative walk from kLook bytes before the segment
         if (a >= blk.z && j) {
             sx = pack_pt(k, b, ST_A);
         } else {
@@ -374,218 +369,210 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
                 }
                 if (pos >= a) {
                     const uint32_t bit = 1u << (pos - a);
-                    const uint32_t s = st == ST_F ? ST_A : st;
-                    bm0 |= s == ST_A ? bit : 0u;
-                    bm1 |= s == ST_B ? bit : 0u;
-                    bm2 |= s == ST_C ? bit : 0u;
+                    const uint32_t s2 = st == ST_F ? ST_A : st;
+                    bm0 |= s2 == ST_A ? bit : 0u;
+                    bm1 |= s2 == ST_B ? bit : 0u;
+                    bm2 |= s2 == ST_C ? bit : 0u;
                 }
                 pos = t.pos;
                 st = t.st;
             }
             if (pos >= a && pos < b) {           // stopped inside: the stop point is a start
                 const uint32_t bit = 1u << (pos - a);
-                const uint32_t s = st == ST_F ? ST_A : st;
-                bm0 |= s == ST_A ? bit : 0u;
-                bm1 |= s == ST_B ? bit : 0u;
-                bm2 |= s == ST_C ? bit : 0u;
+                const uint32_t s2 = st == ST_F ? ST_A : st;
+                bm0 |= s2 == ST_A ? bit : 0u;
+                bm1 |= s2 == ST_B ? bit : 0u;
+                bm2 |= s2 == ST_C ? bit : 0u;
             }
             sx = pack_pt(k, pos, st);
         }
-        L.ex[0][j] = sx;
-    }
+        STAMP(1);
 
-    auto in_bm = [&](uint32_t pos, uint32_t st) -> bool {
-        if (pos < a || pos >= b)
-            return false;
-        const uint32_t s = st == ST_F ? ST_A : st;
-        const uint32_t m = s == ST_A ? bm0 : s == ST_B ? bm1 : bm2;
-        return (m >> (pos - a)) & 1u;
-    };
-    // exit of this lane's segment from a true entry (packed)
-    auto exit_from = [&](uint32_t ent) -> uint32_t {
-        uint32_t pos = I + (ent >> 2), st = ent & 3u;
-        if (pos >= b)
-            return ent;
-        if (in_bm(pos, st))
-            return sx;
-        for (;;) {
-            const Tok t = tok(L, k, pos, st);
-            if (t.fl)
-                return pack_pt(k, pos, st);      // stop point
-            pos = t.pos;
-            st = t.st;
-            if (pos >= b)
-                return pack_pt(k, pos, st);
-            if (in_bm(pos, st))
-                return sx;
-        }
-    };
+        auto in_bm = [&](uint32_t key) -> bool {
+            const uint32_t pos = I + (key >> 2), st = key & 3u;
+            if (pos < a || pos >= b)
+                return false;
+            const uint32_t s2 = st == ST_F ? ST_A : st;
+            const uint32_t m = s2 == ST_A ? bm0 : s2 == ST_B ? bm1 : bm2;
+            return (m >> (pos - a)) & 1u;
+        };
 
-    // P2: exits from true entries.  Inside each parse wave the exits settle by
-    // Jacobi steps over the lanes (entry = the lane below's exit, by shuffle;
-    // a lane re-walks only when its entry changed), no barrier; then wave 1
-    // settles again once wave 0's last exit is known.
-    const uint32_t lane = lane_id();
-    uint32_t my_ent = kNone, my_ex = sx;
-    auto settle = [&](uint32_t lane0_entry) {
-        for (;;) {
-            uint32_t e = (uint32_t)__shfl_up((int)my_ex, 1, kWave);
-            if (lane == 0)
-                e = lane0_entry;
-            bool ch = false;
-            if (e != my_ent) {
-                my_ent = e;
-                const uint32_t nx = exit_from(e);
-                ch = nx != my_ex;
-                my_ex = nx;
+        // P2: settle the exits from the true entries.  ok: this lane's exit is
+        // its speculative one whenever its predecessor's is.  A frontier f
+        // moves over the lanes: runs of ok lanes are taken at once (ballot),
+        // entries past a segment pass over it, and only a lane whose true
+        // entry is not one of its speculative starts walks.
+        const uint32_t psx = (uint32_t)__shfl_up((int)sx, 1, kWave);
+        const uint64_t okm = __ballot(j > 0 && in_bm(psx));
+        uint32_t x = sx;
+        uint32_t f = 1, cur = uni(__builtin_amdgcn_readlane(sx, 0));
+        while (f < kWave) {
+            const uint32_t cpos = I + (cur >> 2);
+            const uint32_t af = I + kG * f;
+            if (cpos < af) {                     // a stop point: no starts after it
+                x = j >= f ? cur : x;
+                break;
+            }
+            if (cpos >= af + kG) {               // passes over lanes f .. g-1
+                uint32_t g = (cpos - I) / kG;
+                g = g < kWave ? g : kWave;
+                x = (j >= f && j < g) ? cur : x;
+                f = g;
+                continue;
             }
             COUNT(12, 1);
-            if (__ballot(ch) == 0ull)
-                break;
+            const uint64_t hit = __ballot(in_bm(cur));
+            if ((hit >> f) & 1ull) {
+                // lanes f .. g-1 keep their speculative exits
+                const uint64_t rest = f + 1 < kWave ? ~okm & (~0ull << (f + 1)) : 0ull;
+                const uint32_t g = rest ? (uint32_t)__builtin_ctzll(rest) : kWave;
+                cur = uni(__builtin_amdgcn_readlane(sx, g - 1));
+                f = g;
+            } else {
+                uint32_t w = 0;
+                if (j == f) {                    // walk from the true entry
+                    uint32_t pos = cpos, st = cur & 3u;
+                    for (;;) {
+                        const Tok t = tok(L, k, pos, st);
+                        if (t.fl) {
+                            w = pack_pt(k, pos, st);
+                            break;
+                        }
+                        pos = t.pos;
+                        st = t.st;
+                        if (pos >= b) {
+                            w = pack_pt(k, pos, st);
+                            break;
+                        }
+                        const uint32_t key = pack_pt(k, pos, st);
+                        if (in_bm(key)) {
+                            w = sx;
+                            break;
+                        }
+                    }
+                    x = w;
+                }
+                cur = uni(__builtin_amdgcn_readlane(w, f));
+                f++;
+            }
         }
-    };
-    __syncthreads();                             // spec exits in ex[0]
-    STAMP(1);
-    uint32_t w1_entry = 0;
-    if (pl) {
-        w1_entry = L.ex[0][kWave - 1];           // wave 1 starts from wave 0's spec exit
-        settle(tid < kWave ? entry0 : w1_entry);
-        L.ex[1][j] = my_ex;
-    }
-    __syncthreads();
-    if (pl && tid >= kWave) {
-        const uint32_t e63 = L.ex[1][kWave - 1];
-        if (e63 != w1_entry) {                   // wave-uniform
-            settle(e63);
-            L.ex[1][j] = my_ex;
-        }
-    }
-    __syncthreads();
-    STAMP(2);
-    const uint32_t fin = 1;                      // ex[1] holds the settled exits
-    const uint32_t ent = pl ? (j ? L.ex[fin][j - 1] : entry0) : 0u;
+        STAMP(2);
 
-    // P3: count ops and bytes on the true path
-    uint32_t c_ops = 0, c_bytes = 0, skind = 0, spos = 0, sst = 0;
-    if (pl) {
-        uint32_t pos = I + (ent >> 2), st = ent & 3u;
-        while (pos < b) {
-            const Tok t = tok(L, k, pos, st);
-            if (t.fl) {
-                skind = t.fl;
-                spos = pos;
-                sst = st;
-                break;
+        // P3: count ops and bytes on the true path
+        uint32_t ent = (uint32_t)__shfl_up((int)x, 1, kWave);
+        if (j == 0)
+            ent = entry0;
+        uint32_t c_ops = 0, c_bytes = 0, skind = 0, spos = 0, sst = 0;
+        {
+            uint32_t pos = I + (ent >> 2), st = ent & 3u;
+            if (pos >= a) {
+                while (pos < b) {
+                    const Tok t = tok(L, k, pos, st);
+                    if (t.fl) {
+                        skind = t.fl;
+                        spos = pos;
+                        sst = st;
+                        break;
+                    }
+                    c_ops += (t.aL ? 1u : 0u) + (t.bL ? 1u : 0u);
+                    c_bytes += t.aL + t.bL;
+                    pos = t.pos;
+                    st = t.st;
+                }
             }
-            c_ops += (t.aL ? 1u : 0u) + (t.bL ? 1u : 0u);
-            c_bytes += t.aL + t.bL;
-            pos = t.pos;
-            st = t.st;
         }
-        if (skind)
-            atomicMin(&L.ctl[C_STOPLANE], j);
-    }
-    // scan over the two parse waves
-    const uint32_t wave = tid >> 6;
-    (void)lane;
-    const uint32_t i_ops = wave_incl_scan(c_ops), i_bytes = wave_incl_scan(c_bytes);
-    if (tid == 63) {
-        L.wsum[0] = i_ops;
-        L.wsum[1] = i_bytes;
-    }
-    __syncthreads();
-    STAMP(3);
-    const uint32_t b_ops = i_ops - c_ops + (wave == 1 ? L.wsum[0] : 0u);
-    const uint32_t b_bytes = i_bytes - c_bytes + (wave == 1 ? L.wsum[1] : 0u);
-    const uint32_t stoplane = L.ctl[C_STOPLANE];
-    if (pl && j == stoplane) {
-        L.ctl[C_SPOS] = spos;
-        L.ctl[C_SST] = sst;
-        L.ctl[C_SKIND] = skind;
-    }
-    if (tid == kNPL - 1) {
-        L.ctl[C_TOPS] = b_ops + c_ops;
-        L.ctl[C_TBYTES] = b_bytes + c_bytes;
-    }
+        const uint32_t i_ops = wave_incl_scan(c_ops), i_bytes = wave_incl_scan(c_bytes);
+        const uint32_t b_ops = i_ops - c_ops, b_bytes = i_bytes - c_bytes;
+        const uint32_t t_ops = uni(__builtin_amdgcn_readlane(i_ops, kWave - 1));
+        const uint32_t t_bytes = uni(__builtin_amdgcn_readlane(i_bytes, kWave - 1));
+        const uint64_t stops = __ballot(skind != 0);
+        STAMP(3);
 
-    // literal source: a zin offset when the bytes are staged, else the input
-    // position (long literal runs past the piece are read from HBM)
-    auto lit_src = [&](uint32_t q, uint32_t n) -> uint32_t {
-        return q + n <= k.sEnd ? kLitF | (k.zb + (q - I)) : kLitF | kLitG | q;
-    };
-    // P4: emit ops (stop at the op cap: that instruction starts the next piece)
-    const uint32_t avail = kOpCap - nops;
-    if (pl && c_ops && b_ops <= avail) {
-        uint32_t pos = I + (ent >> 2), st = ent & 3u;
-        uint32_t n = b_ops, outp = E + b_bytes;
-        while (pos < b) {
-            const Tok t = tok(L, k, pos, st);
-            if (t.fl)
-                break;
-            const uint32_t need = (t.aL ? 1u : 0u) + (t.bL ? 1u : 0u);
-            if (n + need > avail) {
-                L.ctl[C_CUTLANE] = j;
-                L.ctl[C_CUTPOS] = pos;
-                L.ctl[C_CUTST] = st;
-                L.ctl[C_CUTOPS] = n;
-                L.ctl[C_CUTBYTES] = outp - E;
-                break;
+        // literal source: a zin offset when the bytes are staged, else the input
+        // position (long literal runs past the piece are read from HBM)
+        auto lit_src = [&](uint32_t q, uint32_t n) -> uint32_t {
+            return q + n <= k.sEnd ? kLitF | (k.zb + (q - I)) : kLitF | kLitG | q;
+        };
+        // P4: emit ops; at the op cap the instruction that does not fit starts
+        // the next piece
+        const uint32_t avail = kOpCap - nops;
+        const uint64_t over = __ballot(b_ops + c_ops > avail);
+        uint32_t cut_pos = 0, cut_st = 0, cut_n = 0, cut_out = 0;
+        if (c_ops && b_ops <= avail) {
+            uint32_t pos = I + (ent >> 2), st = ent & 3u;
+            uint32_t n = b_ops, outp = E + b_bytes;
+            while (pos < b) {
+                const Tok t = tok(L, k, pos, st);
+                if (t.fl)
+                    break;
+                const uint32_t need = (t.aL ? 1u : 0u) + (t.bL ? 1u : 0u);
+                if (n + need > avail) {
+                    cut_pos = pos;
+                    cut_st = st;
+                    cut_n = n;
+                    cut_out = outp;
+                    break;
+                }
+                if (t.aL) {
+                    L.opp[nops + n] = outp;
+                    L.ops[nops + n] = (t.aS & kLitF) ? lit_src(t.aS & ~kLitF, t.aL) : t.aS;
+                    n++;
+                    outp += t.aL;
+                }
+                if (t.bL) {
+                    L.opp[nops + n] = outp;
+                    L.ops[nops + n] = lit_src(t.bS & ~kLitF, t.bL);
+                    n++;
+                    outp += t.bL;
+                }
+                pos = t.pos;
+                st = t.st;
             }
-            if (t.aL) {
-                L.opp[nops + n] = outp;
-                L.ops[nops + n] = (t.aS & kLitF) ? lit_src(t.aS & ~kLitF, t.aL) : t.aS;
-                n++;
-                outp += t.aL;
-            }
-            if (t.bL) {
-                L.opp[nops + n] = outp;
-                L.ops[nops + n] = lit_src(t.bS & ~kLitF, t.bL);
-                n++;
-                outp += t.bL;
-            }
-            pos = t.pos;
-            st = t.st;
         }
-    }
-    __syncthreads();
-    STAMP(4);
-
-    PieceOut r;
-    if (L.ctl[C_CUTLANE] != kNone) {
-        r.result = PR_FULL;
-        r.I = L.ctl[C_CUTPOS];
-        r.st = L.ctl[C_CUTST];
-        r.nops = nops + L.ctl[C_CUTOPS];
-        r.E = E + L.ctl[C_CUTBYTES];
-    } else {
-        r.nops = nops + L.ctl[C_TOPS];
-        r.E = E + L.ctl[C_TBYTES];
-        if (stoplane != kNone) {
-            const uint32_t sk = L.ctl[C_SKIND];
-            r.I = L.ctl[C_SPOS];
-            r.st = L.ctl[C_SST];
-            r.result = (sk & TK_BAD) ? PR_REFUSE : (sk & TK_EOF) ? PR_EOF : PR_OK;
-            if (sk & TK_EOF)
-                r.I = blk.z;
+        if (over) {
+            const uint32_t cl = (uint32_t)__builtin_ctzll(over);
+            r.result = PR_FULL;
+            r.I = uni(__builtin_amdgcn_readlane(cut_pos, cl));
+            r.st = uni(__builtin_amdgcn_readlane(cut_st, cl));
+            r.nops = nops + uni(__builtin_amdgcn_readlane(cut_n, cl));
+            r.E = uni(__builtin_amdgcn_readlane(cut_out, cl));
         } else {
-            const uint32_t x = L.ex[fin][kNPL - 1];
-            r.I = I + (x >> 2);
-            r.st = x & 3u;
-            r.result = PR_OK;
+            r.nops = nops + t_ops;
+            r.E = E + t_bytes;
+            if (stops) {
+                const uint32_t sl = (uint32_t)__builtin_ctzll(stops);
+                const uint32_t sk = uni(__builtin_amdgcn_readlane(skind, sl));
+                r.I = uni(__builtin_amdgcn_readlane(spos, sl));
+                r.st = uni(__builtin_amdgcn_readlane(sst, sl));
+                r.result = (sk & TK_BAD) ? PR_REFUSE : PR_EOF;
+                if (sk & TK_EOF)
+                    r.I = blk.z;
+            } else {
+                const uint32_t xl = uni(__builtin_amdgcn_readlane(x, kWave - 1));
+                r.I = I + (xl >> 2);
+                r.st = xl & 3u;
+                r.result = PR_OK;
+            }
+        }
+        if (r.result == PR_OK && r.I == I)
+            r.result = PR_REFUSE;                // (never: a piece always starts an instruction)
+        if (j == 0) {
+            L.opp[r.nops] = r.E;                 // sentinel
+            L.ctl[C_SPOS] = r.I;
+            L.ctl[C_SST] = r.st;
+            L.ctl[C_TOPS] = r.nops;
+            L.ctl[C_TBYTES] = r.E;
+            L.ctl[C_SKIND] = r.result;
         }
     }
-    if (r.result == PR_OK && r.I == I)
-        r.result = PR_REFUSE;                    // an instruction longer than a piece
-    r.I = uni(r.I);
-    r.st = uni(r.st);
-    r.nops = uni(r.nops);
-    r.E = uni(r.E);
-    r.result = uni(r.result);
-    if (tid == 0)
-        L.opp[r.nops] = r.E;                     // sentinel
     COUNT(10, 1);
     __syncthreads();
     STAMP(4);
+    r.I = uni(L.ctl[C_SPOS]);
+    r.st = uni(L.ctl[C_SST]);
+    r.nops = uni(L.ctl[C_TOPS]);
+    r.E = uni(L.ctl[C_TBYTES]);
+    r.result = uni(L.ctl[C_SKIND]);
     return r;
 }
 
@@ -664,7 +651,6 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
     if (bad)
         L.ctl[C_REFUSE] = 1;
     // pointer table slice (8 x u16 = 16 B, 16-aligned)
-    uint16_t* const ring16 = (uint16_t*)L.ring;
     {
         uint4 w;
         w.x = e[0] | (e[1] << 16);
@@ -694,26 +680,38 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
     if (L.ctl[C_REFUSE])
         return false;
 
-    // chase in-window sources (pointer table shared, written back as we go)
+    // chase in-window sources (pointer table shared, written back as we go;
+    // relaxed LDS atomics: another lane's entry is read as it is, old or new,
+    // and every value ever stored there is a valid source for its byte)
     {
+        uint32_t* const t32 = (uint32_t*)L.ring;
+        const uint32_t myw = ((tabb + 2 * o) & 0xFFFFu) >> 2;
         bool any = true;
-        volatile uint16_t* const vt = (volatile uint16_t*)ring16;
         while (__ballot(any) != 0ull) {
             any = false;
+            uint32_t w8[8];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; i++) {
+                const uint32_t x = x0 + i;
+                const bool pend = x >= S && x < Ew && e[i] <= T;
+                const uint32_t byteoff = (tabb + 2 * (kW - 1 - (pend ? e[i] : 0u))) & 0xFFFFu;
+                w8[i] = pend ? __hip_atomic_load(&t32[byteoff >> 2], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP) >> (8 * (byteoff & 2))
+                             : 0u;
+            }
 #pragma unroll
             for (uint32_t i = 0; i < 8; i++) {
                 const uint32_t x = x0 + i;
                 if (x >= S && x < Ew && e[i] <= T) {
-                    e[i] = vt[((tabb + 2 * (kW - 1 - e[i])) & 0xFFFFu) >> 1];
+                    e[i] = w8[i] & 0xFFFFu;
                     any |= e[i] <= T;
                 }
             }
             COUNT(11, 1);
-            volatile uint32_t* const vw = (volatile uint32_t*)&L.ring[(tabb + 2 * o) & 0xFFFFu];
-            vw[0] = e[0] | (e[1] << 16);
-            vw[1] = e[2] | (e[3] << 16);
-            vw[2] = e[4] | (e[5] << 16);
-            vw[3] = e[6] | (e[7] << 16);
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++)
+                __hip_atomic_store(&t32[myw + q], e[2 * q] | (e[2 * q + 1] << 16), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();

@@ -13,8 +13,12 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { W = 4096, ZH = 2048, ZR = 2 * ZH, OPCAP = 1024, RING = 65536, G = 16, NPL = ZH / G,
-       LOOK = 16, LITBASE = RING - ZR, NT = 512 };
+enum { W = 4096, ZH = 2048, ZR = 2 * ZH, OPCAP = 1024, RING = 65536, GMAX = 64, NPLMAX = ZH / 4,
+       LITBASE = RING - ZR, NT = 512 };
+static uint32_t G = 16, NPL = ZH / 16, LOOK = 16;
+static long st_spec_tokens, st_fix_tokens, st_rounds, st_lanes, st_div;
+void win_params(uint32_t g, uint32_t look) { G = g; NPL = ZH / g; LOOK = look; st_spec_tokens = st_fix_tokens = st_rounds = st_lanes = st_div = 0; }
+void win_pstats(long out[5]) { out[0] = st_spec_tokens; out[1] = st_fix_tokens; out[2] = st_rounds; out[3] = st_lanes; out[4] = st_div; }
 enum { ST_A = 0, ST_B = 1, ST_C = 2, ST_F = 3 };
 #define LITF 0x80000000u
 
@@ -113,10 +117,11 @@ check:
     return r;
 }
 
-static int in_bm(const uint32_t bm[3], uint32_t a, uint32_t pos, uint32_t st)
+static int in_bm(const uint32_t bm[6], uint32_t a, uint32_t pos, uint32_t st)
 {
     if (pos < a || pos >= a + G) return 0;
-    return (bm[st == ST_F ? ST_A : st] >> (pos - a)) & 1;
+    uint32_t q = pos - a;
+    return (bm[(st == ST_F ? ST_A : st) * 2 + (q >> 5)] >> (q & 31)) & 1;
 }
 
 /* ---- piece parse --------------------------------------------------------- */
@@ -129,12 +134,13 @@ static int parse_piece(M *m, uint32_t *pI, uint32_t *pst, uint32_t *pE, uint32_t
     for (uint32_t i = 0; i < ZH; i++)
         m->zin[half * ZH + i] = (I + i < m->z) ? m->in[I + i] : 0;
     /* P1 speculative walks */
-    uint32_t bm[NPL][3], xpos[NPL], xst[NPL], spos[NPL], sst[NPL];
+    static uint32_t bm[NPLMAX][6], xpos[NPLMAX], xst[NPLMAX], spos[NPLMAX], sst[NPLMAX];
     for (uint32_t j = 0; j < NPL; j++) {
         uint32_t a = I + G * j, b = a + G;
         uint32_t pos = j ? (a >= I + LOOK ? a - LOOK : I) : I, st = j ? ST_A : *pst;
-        bm[j][0] = bm[j][1] = bm[j][2] = 0;
+        memset(bm[j], 0, sizeof(bm[j]));
         uint32_t restart = pos;
+        st_lanes++;
         for (;;) {
             if (pos >= b) break;
             Tok t = decode(m, I, pos, st);
@@ -143,47 +149,64 @@ static int parse_piece(M *m, uint32_t *pI, uint32_t *pst, uint32_t *pE, uint32_t
                 /* impossible guess: restart one byte later */
                 restart++;
                 pos = restart; st = ST_A;
-                bm[j][0] = bm[j][1] = bm[j][2] = 0;
+                memset(bm[j], 0, sizeof(bm[j]));
                 continue;
             }
-            if (pos >= a) bm[j][st == ST_F ? ST_A : st] |= 1u << (pos - a);
+            st_spec_tokens++;
+            if (pos >= a) { uint32_t q = pos - a; bm[j][(st == ST_F ? ST_A : st) * 2 + (q >> 5)] |= 1u << (q & 31); }
             pos = t.pos; st = t.st;
         }
         xpos[j] = spos[j] = pos; xst[j] = sst[j] = st;
-        if (pos >= a && pos < b) /* stopped inside: mark the stop point as a start */
-            bm[j][st == ST_F ? ST_A : st] |= 1u << (pos - a);
+        if (pos >= a && pos < b) { /* stopped inside: mark the stop point as a start */
+            uint32_t q = pos - a; bm[j][(st == ST_F ? ST_A : st) * 2 + (q >> 5)] |= 1u << (q & 31); }
     }
-    /* P2 fix-up: exits from true entries */
-    uint32_t epos[NPL], est[NPL];
-    int changed = 1, it = 0;
-    for (uint32_t j = 0; j < NPL; j++) { epos[j] = ~0u; est[j] = 0; }
+    /* P2 fix-up (kernel round 3b): exits as keys (pos - I) << 2 | st, + 1;
+     * 0 = PASS (the lane has no instruction start on the true path: its entry
+     * passes over it, or is a stop point from an earlier lane).  A lane's entry
+     * is the prefix maximum of the exits below it (true exits increase along
+     * the lanes), so pass-through and stop chains settle in one round. */
+    static uint64_t xk[NPLMAX], ok_[NPLMAX], ent_[NPLMAX];
+    for (uint32_t j = 0; j < NPL; j++) {
+        uint32_t a = I + G * j;
+        xk[j] = (j && a >= m->z) ? 0 : ((uint64_t)(spos[j] - I) << 2 | sst[j]) + 1;
+        ent_[j] = ~0ull;
+    }
+    int changed = 1;
     while (changed) {
-        changed = 0; it++;
+        changed = 0; st_rounds++;
+        memcpy(ok_, xk, sizeof(uint64_t) * NPL);           /* Jacobi */
+        uint64_t run = 0;
         for (uint32_t j = 1; j < NPL; j++) {
-            uint32_t pp = xpos[j - 1], ps = xst[j - 1];
-            if (pp == epos[j] && ps == est[j]) continue;
-            epos[j] = pp; est[j] = ps;
+            run = ok_[j - 1] > run ? ok_[j - 1] : run;
+            if (run == ent_[j]) continue;
+            ent_[j] = run;
             uint32_t a = I + G * j, b = a + G;
-            uint32_t pos = pp, st = ps, nx, ns;
-            if (pos >= b) { nx = pos; ns = st; }
-            else if (in_bm(bm[j], a, pos, st)) { nx = spos[j]; ns = sst[j]; }  /* synced */
+            uint32_t pos = I + (uint32_t)((run - 1) >> 2), st = (uint32_t)((run - 1) & 3);
+            uint64_t nk;
+            if (run == 0 || pos < a || pos >= b) nk = 0;              /* pass / stop propagation */
+            else if (in_bm(bm[j], a, pos, st)) nk = ((uint64_t)(spos[j] - I) << 2 | sst[j]) + 1;
             else {
                 m->walks_fix++;
+                int landed = 0;
                 for (;;) {
                     if (pos >= b) break;
-                    if (in_bm(bm[j], a, pos, st)) {
-                        /* landed on a speculative start: spec exit holds */
-                        pos = ~0u;
-                        break;
-                    }
+                    if (in_bm(bm[j], a, pos, st)) { landed = 1; break; }
                     Tok t = decode(m, I, pos, st);
+                    st_fix_tokens++;
                     if (t.bad || t.cut || t.eof) break;
                     pos = t.pos; st = t.st;
                 }
-                if (pos == ~0u) { nx = spos[j]; ns = sst[j]; }
-                else { nx = pos; ns = st; }
+                nk = landed ? ((uint64_t)(spos[j] - I) << 2 | sst[j]) + 1 : ((uint64_t)(pos - I) << 2 | st) + 1;
             }
-            if (nx != xpos[j] || ns != xst[j]) { xpos[j] = nx; xst[j] = ns; changed = 1; }
+            if (nk != xk[j]) { xk[j] = nk; changed = 1; }
+        }
+    }
+    /* resolved exits (prefix max) for the check below */
+    {
+        uint64_t run = 0;
+        for (uint32_t j = 0; j < NPL; j++) {
+            run = xk[j] > run ? xk[j] : run;
+            xpos[j] = I + (uint32_t)((run - 1) >> 2); xst[j] = (uint32_t)((run - 1) & 3);
         }
     }
     /* P3/P4: walk true paths, emit ops in lane order (sequential here) */
@@ -191,6 +214,7 @@ static int parse_piece(M *m, uint32_t *pI, uint32_t *pst, uint32_t *pE, uint32_t
     int rc = 0;
     for (uint32_t j = 0; j < NPL; j++) {
         uint32_t b = I + G * (j + 1);
+        uint32_t lane_ent_pos = pos;
         while (pos < b) {
             Tok t = decode(m, I, pos, st);
             if (t.cut) goto done;            /* reads past the staged piece first */
@@ -213,6 +237,10 @@ static int parse_piece(M *m, uint32_t *pI, uint32_t *pst, uint32_t *pE, uint32_t
                 m->nops++; E += t.bL;
             }
             pos = t.pos; st = t.st;
+        }
+        { /* divergence: true exit differs from the speculative one (pass-through excluded) */
+            uint32_t a = I + G * j;
+            if (lane_ent_pos >= a && lane_ent_pos < b && (pos != spos[j] || st != sst[j])) st_div++;
         }
         /* check the parallel exits agree with the sequential walk */
         if (pos != xpos[j] || st != xst[j]) {
