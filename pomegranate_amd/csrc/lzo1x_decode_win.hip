@@ -59,7 +59,7 @@ constexpr uint32_t kLitF = 0x80000000u;          // op source: literal ...
 constexpr uint32_t kLitG = 0x40000000u;          // ... at an input position (else a zin offset)
 constexpr int32_t kFallback = 0x7FFF0001;
 static_assert(kW * 8 == kNT * 64, "window: 8 bytes per thread");
-static_assert(2 * kW <= 65536u - 0xBFFFu - 1u, "pointer table slots must be dead ring slots");
+static_assert(kW + 2 * kW <= 65536u - 0xBFFFu - 1u, "pointer table [A+W, A+3W) in dead ring slots");
 static_assert(0xBFFFu + kW < kFin && kFin + kW <= 65536u, "e encoding: match pointers below final ones");
 static_assert(kNPL == kWave, "one parse wave");
 
@@ -577,27 +577,38 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
 }
 
 // ---- window -------------------------------------------------------------------
+// Op starts in (S, A + W) into the bitmap bm (positions relative to A).
+__device__ __forceinline__ void scatter_starts(WinLds& L, uint32_t* bm, uint32_t A, uint32_t iS,
+                                               uint32_t nops)
+{
+    for (uint32_t i = iS + 1 + threadIdx.x; i < nops; i += kNT) {
+        const uint32_t p = L.opp[i];
+        if (p >= A + kW)
+            break;
+        atomicOr(&bm[(p - A) >> 5], 1u << ((p - A) & 31u));
+    }
+}
+
 // Output [S, Ew) with the thread grid anchored at A = S & ~15 (bytes of the grid
 // below S or at/after Ew are rewritten with their own ring bytes).  Returns
-// false on a lookbehind error.  *iS: index of the op covering S, updated to
-// the op covering Ew.
+// false on a lookbehind error.  iS: index of the op covering S, updated to the
+// op covering Ew.  Two barriers: after the pointer table (and the literal
+// bytes) are written, and at the end; the op-start bitmap of the next window
+// is filled during this one when that window follows in the same piece
+// (next_same), else at the start of the next one (prepped false).
 template <bool STAMPS>
 __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, uint32_t& iS,
-                                           uint32_t nops, uint32_t& cur)
+                           uint32_t nops, uint32_t& cur, bool& prepped, bool next_same)
 {
     const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
     const uint32_t A = S & ~15u, B = A + kW - 1, T = B - S;
     const uint32_t tabb = A + kW;               // tab[i] at ring[(tabb + 2i) & 0xFFFF]
     uint32_t* const bm = L.bmap[cur];
 
-    // op starts in (S, A + W) -> bitmap
-    for (uint32_t i = iS + 1 + tid; i < nops; i += kNT) {
-        const uint32_t p = L.opp[i];
-        if (p >= A + kW)
-            break;
-        atomicOr(&bm[(p - A) >> 5], 1u << ((p - A) & 31u));
+    if (!prepped) {
+        scatter_starts(L, bm, A, iS, nops);
+        __syncthreads();
     }
-    __syncthreads();
     STAMP(5);
 
     const uint32_t o = wave * 512 + lane * 8;    // this thread's 8 bytes: A + o ..
@@ -672,13 +683,20 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
         w.y = (w.y & ~m1) | (lv1 & m1);
         *slot = w;
     }
-    // clear the other bitmap for the next window
-    if (tid < kW / 32)
-        L.bmap[cur ^ 1u][tid] = 0;
+    // op covering Ew; the next window's op starts
+    uint32_t nx = iS + total;
+    if (nx + 1 < nops && L.opp[nx + 1] <= Ew)
+        nx++;
+    nx = uni(nx);
+    if (next_same)
+        scatter_starts(L, L.bmap[cur ^ 1u], Ew & ~15u, nx, nops);
     __syncthreads();
     STAMP(6);
     if (L.ctl[C_REFUSE])
         return false;
+    // this window's bitmap is read: clear it for the window after next
+    if (tid < kW / 32)
+        bm[tid] = 0;
 
     // chase in-window sources (pointer table shared, written back as we go;
     // relaxed LDS atomics: another lane's entry is read as it is, old or new,
@@ -714,10 +732,11 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
-    __syncthreads();
     STAMP(7);
 
-    // gather
+    // gather (no barrier after the chase: a lane's final sources are literal
+    // bytes, written before the barrier above, or bytes before S; the ring
+    // bytes written below are never a final source of this window)
     uint32_t lo = 0, hi = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 8; i++) {
@@ -730,7 +749,6 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
         else
             hi |= v << (8 * (i - 4));
     }
-    // (no barrier: the ring bytes written here are never a final source)
     *(uint2*)&L.ring[x0 & 0xFFFFu] = make_uint2(lo, hi);
     if (x0 >= S && x0 + 8 <= Ew) {
         *(uint2*)(blk.out + x0) = make_uint2(lo, hi);
@@ -742,14 +760,11 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
                 blk.out[x] = (uint8_t)((i < 4 ? lo >> (8 * i) : hi >> (8 * (i - 4))) & 0xFFu);
         }
     }
-    // op covering Ew
-    uint32_t nx = iS + total;
-    if (nx + 1 < nops && L.opp[nx + 1] <= Ew)
-        nx++;
-    iS = uni(nx);
+    iS = nx;
     cur ^= 1u;
+    prepped = next_same;
     COUNT(9, 1);
-    __syncthreads();
+    __syncthreads();          // ring bytes final; every chase done before the next table
     STAMP(8);
     return true;
 }
@@ -842,9 +857,11 @@ __global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
         nops = r.nops;
         E = r.E;
         const bool eof = r.result == PR_EOF;
-        while (S < E && ((S & ~15u) + kW <= E || eof)) {
+        auto full_next = [&](uint32_t s2) { return s2 < E && ((s2 & ~15u) + kW <= E || eof); };
+        bool prepped = false;
+        while (full_next(S)) {
             const uint32_t Ew = (S & ~15u) + kW < E ? (S & ~15u) + kW : E;
-            if (!run_window<STAMPS>(L, blk, S, Ew, iS, nops, cur)) {
+            if (!run_window<STAMPS>(L, blk, S, Ew, iS, nops, cur, prepped, full_next(Ew))) {
                 ok = false;
                 break;
             }
@@ -855,7 +872,8 @@ __global__ __launch_bounds__(kNT, 4) void lzo1x_decode_win_kernel(
         if (eof)
             break;
         if (S < E && (S < Pk || r.result == PR_FULL)) {
-            if (!run_window<STAMPS>(L, blk, S, E, iS, nops, cur)) {
+            bool prepped2 = false;
+            if (!run_window<STAMPS>(L, blk, S, E, iS, nops, cur, prepped2, false)) {
                 ok = false;
                 break;
             }
