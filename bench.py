@@ -361,6 +361,48 @@ class Resident:
                  for d, _, st, _, _ in self._pipe)
         return wall, ok
 
+    def roundtrip_pipelined(self, steps, warmup=2):
+        """Wall time of `steps` C3 round trips (compress, then decompress what it
+        produced) issued back to back on two streams, each stream with its own
+        compressed image, output and scratch: one round trip's decode overlaps
+        the next one's encode.  Every round trip keeps its data dependence; the
+        outputs of both streams are checked."""
+        torch, lzo = self.torch, self.lzo
+        if not hasattr(self, "_rt"):
+            sets = []
+            for i in range(2):
+                if i == 0:
+                    zd, zl, zs, od, ol, os_, scr, cscr = (self.zdst, self.zlen, self.zst, self.odst,
+                                                           self.olen, self.ost, self.scratch,
+                                                           self.cscratch)
+                else:
+                    za = torch.empty_like(self.zdst.arena)
+                    zd = lzo.DeviceBatch(za, self.zdst.off, self.zdst.length)
+                    zl, zs = torch.zeros_like(self.zlen), torch.zeros_like(self.zst)
+                    od = lzo.DeviceBatch(torch.zeros_like(self.out), self.src.off, self.src.length)
+                    ol, os_ = torch.zeros_like(self.olen), torch.zeros_like(self.ost)
+                    scr, cscr = torch.empty_like(self.scratch), torch.empty_like(self.cscratch)
+                zsrc = lzo.DeviceBatch(zd.arena, zd.off, zl)
+                sets.append((zd, zl, zs, zsrc, od, ol, os_, scr, cscr, torch.cuda.Stream()))
+            self._rt = sets
+
+        def step(i):
+            zd, zl, zs, zsrc, od, ol, os_, scr, cscr, s = self._rt[i & 1]
+            lzo.compress_dev(self.src, zd, zl, zs, stream=s, scratch=cscr)
+            lzo.decompress_dev(zsrc, od, ol, os_, scr, stream=s)
+        torch.cuda.synchronize()
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ok = all(torch.equal(od.arena, self.src.arena) and bool((os_ == 0).all()) and bool((zs == 0).all())
+                 for _, _, zs, _, od, _, os_, _, _, _ in self._rt)
+        return wall, ok
+
     def errors(self):
         torch = self.torch
         e = int((self.zst != 0).sum().item()) + int((self.ost != 0).sum().item())
@@ -537,6 +579,13 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
         result["decompress_pipelined_gibps"] = round(n_all * args.steps / p_wall / GIB, 3)
         result["decompress_pipelined_exact"] = p_ok
         errors += 0 if p_ok else 1
+        if args.workload == "c3":
+            # round trips on two streams: one's decode beside the next one's
+            # encode (reported beside `value`, which runs them one at a time)
+            r_wall, r_ok = R.roundtrip_pipelined(args.steps)
+            result["roundtrip_pipelined_gibps"] = round(n_all * args.steps / r_wall / GIB, 3)
+            result["roundtrip_pipelined_exact"] = r_ok
+            errors += 0 if r_ok else 1
         result["errors"] = errors
     if rank == 0 and world == 1 and not args.no_cpu and args.workload in ("c2", "c3"):
         plain, comps = R.sample(min(len(mine), 512))

@@ -236,15 +236,37 @@ size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
     return scr_ops_off(nblocks) + scr_sets(nblocks) * lzo_mi355x_fast_ops_bytes_per_block();
 }
 
-/* Which throughput decoder runs: the windowed one (lzo1x_decode_win.hip,
- * default) or the round-2 op-set decoder (lzo1x_decode_fast.hip) with
- * POM_DECODER=fast, kept for A/B measurements. */
-static int use_win_decoder(void)
+/* Which throughput decoder a batch uses: the op-set decoder
+ * (lzo1x_decode_fast.hip: 16 blocks per CU) or the windowed one
+ * (lzo1x_decode_win.hip: 2 blocks per CU, a 64 KiB LDS output ring, never
+ * reads its own output back).  POM_DECODER=fast|win forces one; single calls
+ * always use the windowed one (see single_call). */
+static int use_win_decoder(uint32_t nblocks)
 {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("POM_DECODER");
-        v = !(e && strcmp(e, "fast") == 0);
+        v = !e ? 2 : strcmp(e, "win") == 0 ? 1 : 0;
+    }
+    if (v != 2)
+        return v;
+    /* default: the windowed decoder while the batch fits two workgroups per
+     * CU (one round; lone blocks decode 1.3-1.5x faster there), the op-set
+     * decoder for larger batches (16 blocks per CU) */
+    const uint32_t cus = lzo_mi355x_fast_resident_blocks() / 16u;
+    return nblocks <= 2u * (cus ? cus : 256u);
+}
+
+/* Single calls: the kernels write the output and its length/status straight
+ * into the pinned host staging (mapped, coherent: hipHostMalloc's default), so
+ * nothing is copied back but what was produced.  POM_SC_COPY=1: the round-2
+ * path (device staging, one D2H copy of the whole room). */
+static int sc_zero_copy(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("POM_SC_COPY");
+        v = !(e && strcmp(e, "1") == 0);
     }
     return v;
 }
@@ -254,10 +276,24 @@ static int use_win_decoder(void)
  * streams).  Without scratch every block takes the exact decoder.
  * unchecked: the exact decoder follows the unchecked lzo1x_decompress (the
  * fast decoder only ever finishes streams on which both agree). */
+static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                               uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
+                               uint32_t *out_len, int32_t *status, uint32_t nblocks, void *scratch,
+                               int unchecked, int win, hipStream_t s);
+
 static int decompress_dev(const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                           uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
                           uint32_t *out_len, int32_t *status, uint32_t nblocks, void *scratch,
                           int unchecked, hipStream_t s)
+{
+    return decompress_dev_with(src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
+                               nblocks, scratch, unchecked, use_win_decoder(nblocks), s);
+}
+
+static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                               uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
+                               uint32_t *out_len, int32_t *status, uint32_t nblocks, void *scratch,
+                               int unchecked, int win, hipStream_t s)
 {
     if (nblocks == 0)
         return 0;
@@ -268,7 +304,7 @@ static int decompress_dev(const uint8_t *src, const uint64_t *src_off, const uin
     uint8_t *scr = scratch;
     const uint32_t nsets = (uint32_t)scr_sets(nblocks);
     uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nblocks));
-    if (use_win_decoder()) {
+    if (win) {
         /* the windowed decoder: no op sets, only the fallback list */
         if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
             return -1;
@@ -868,6 +904,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
     struct slot *t = single_slot();
     if (!t || src_len > 0xFFFFFFF0u || room > 0xFFFFFFF0u)
         return LZO_E_ERROR;
+    const int zc = sc_zero_copy();
     const size_t o_src = SC_HDR + ALIGN_UP(room, 256);
     const size_t o_scr = o_src + ALIGN_UP(src_len, 256);
     const size_t dneed = o_scr + (kind == SC_COMPRESS ? 0 : lzo_mi355x_decompress_scratch(1));
@@ -881,6 +918,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
     hh->dst_off = SC_HDR;
     hh->src_len = (uint32_t)src_len;
     hh->dst_cap = (uint32_t)room;
+    hh->status = -1;
     if (src_len)
         memcpy(h + o_src, src, src_len);
     struct sc_hdr *dh = (struct sc_hdr *)d;
@@ -890,21 +928,24 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
         (src_len && hipMemcpyAsync(d + o_src, h + o_src, src_len, hipMemcpyHostToDevice, s) !=
                         hipSuccess))
         return LZO_E_ERROR;
+    /* zero copy: output, out_len and status land in the pinned host header/room */
+    uint8_t *out = zc ? h : d;
+    uint32_t *olen = zc ? &hh->out_len : &dh->out_len;
+    int32_t *ost = zc ? &hh->status : &dh->status;
     int rc = 0;
     if (kind == SC_COMPRESS) {
-        rc = lzo_mi355x_compress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
-                                     NULL, s);   /* one block: the LDS dictionary is faster */
-    } else if (kind == SC_SAFE) {
-        rc = decompress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
-                            d + o_scr, 0, s);
+        rc = lzo_mi355x_compress_dev(d, so, sl, out, dof, &dh->dst_cap, olen, ost, 1, NULL,
+                                     s);   /* one block: the LDS dictionary is faster */
     } else {
-        /* decoded into the room; the unchecked decoder never reports an output
-         * overrun (lib/minilzo.c:3676-3680), so OUTPUT_OVERRUN here means the
-         * stream is longer than the room */
-        rc = decompress_dev(d, so, sl, d, dof, &dh->dst_cap, &dh->out_len, &dh->status, 1,
-                            d + o_scr, 1, s);
+        /* SC_UNCHECKED: decoded into the room; the unchecked decoder never
+         * reports an output overrun (lib/minilzo.c:3676-3680), so
+         * OUTPUT_OVERRUN here means the stream is longer than the room.
+         * The windowed decoder never reads its output back (host memory). */
+        rc = decompress_dev_with(d, so, sl, out, dof, &dh->dst_cap, olen, ost, 1, d + o_scr,
+                                 kind == SC_UNCHECKED, 1, s);
     }
-    if (rc != 0 || hipMemcpyAsync(h, d, o_src, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (rc != 0 ||
+        (!zc && hipMemcpyAsync(h, d, o_src, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess)
         return LZO_E_ERROR;
     if (kind == SC_UNCHECKED && hh->status == LZO_E_OUTPUT_OVERRUN) {
@@ -912,7 +953,8 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
          * retries with that much room */
         if (lzo_mi355x_launch_decoded_length(d, so, sl, &dh->plen, &dh->pstatus, 1, NULL,
                                              0xFFFFFFFFu, s) != 0 ||
-            hipMemcpyAsync(h, d, sizeof(*hh), hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(&hh->plen, &dh->plen, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return LZO_E_ERROR;
         if (hh->plen > room) {

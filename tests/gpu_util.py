@@ -89,3 +89,27 @@ def fetch(batch, olen, cap=None) -> List[bytes]:
         n = int(ol[i]) if cap is None else min(int(ol[i]), int(cap[i]))
         res.append(host[int(off[i]): int(off[i]) + n].tobytes())
     return res
+
+
+def gpu_decompress_win(torch, comps: Sequence[bytes], caps: Sequence[int], dev):
+    """The windowed decoder alone (lzo_mi355x_launch_decompress_win): outputs,
+    statuses and the ids of the blocks it handed over (fallback list)."""
+    import ctypes
+    lib = lzo.load()
+    fn = lib.lzo_mi355x_launch_decompress_win
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
+    src = device_batch(torch, comps, dev)
+    dst = empty_batch(torch, caps, dev, fill=0x5A)
+    n = len(comps)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    head = torch.zeros(64, dtype=torch.int32, device=dev)
+    ids = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+    p = lambda x: x.data_ptr()
+    rc = fn(p(src.arena), p(src.off), p(src.length), p(dst.arena), p(dst.off), p(dst.length),
+            p(olen), p(st), p(head), p(ids), n, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    nfb = int(head[0].item())
+    return fetch(dst, olen, cap=caps), st.cpu().numpy().tolist(), sorted(ids[:nfb].cpu().numpy().tolist())

@@ -610,3 +610,62 @@ def test_encoder_block_tickets_mixed_sizes(dev, gu):
     torch.cuda.synchronize()
     assert int((st != 0).sum().item()) == 0
     assert torch.equal(back, src.arena)
+
+
+def test_window_decoder_every_valid_stream(dev, gu):
+    """The windowed decoder (lzo1x_decode_win.hip) alone, without the exact
+    decoder behind it: every content model (incompressible blocks with
+    literal runs far longer than a 2 KiB piece, all-zero blocks with length
+    extensions past a piece), ITB blocks over the C4/C5 size range, the
+    adversarial blocks and a 1 MiB block (the 64 KiB LDS ring wraps 16 times)
+    decode bit-exactly and none is handed over."""
+    blocks = []
+    for kib in (4, 12, 64, 100, 256, 524):
+        blocks += [synth.block(synth.ITB, 3000 * kib + i, kib * 1024 + 7 * i) for i in range(2)]
+    for model in range(6):
+        blocks += [synth.block(model, 6000 + model * 10 + i, n)
+                   for i, n in enumerate((1, 13, 14, 4096, 65536, 300000))]
+    blocks += _long_literal_prefix_blocks()
+    blocks += [b for b in _adversarial_blocks() if b]
+    blocks.append(synth.block(synth.LZLIKE, 77, 1 << 20))
+    comps, st = gu.gpu_compress(torch, blocks, dev)
+    assert all(s == 0 for s in st)
+    outs, st2, handed = gu.gpu_decompress_win(torch, comps, [len(b) for b in blocks], dev)
+    assert handed == []
+    assert st2 == [0] * len(blocks)
+    bad = [i for i, (o, b) in enumerate(zip(outs, blocks)) if o != b]
+    assert not bad, bad[:8]
+
+
+def test_window_decoder_full_grammar_streams(dev, gu):
+    """LZO1X streams the LZO1X-1 compressor never writes (M1 after literal runs
+    and trailing literals, long extensions, first runs of 1-3 bytes) decode
+    bit-exactly on the windowed decoder, none handed over."""
+    import lzo_streams
+    streams = [lzo_streams.stream(2000 + s, [50, 300, 5000, 40000, 150000][s % 5])
+               for s in range(80)]
+    comps = [z for z, _ in streams]
+    want = [o for _, o in streams]
+    outs, st, handed = gu.gpu_decompress_win(torch, comps, [len(o) for o in want], dev)
+    assert handed == []
+    assert st == [0] * len(want)
+    assert outs == want
+
+
+def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, malformed):
+    """Malformed streams, and valid streams whose output does not fit, are
+    handed to the exact decoder (status 0x7FFF0001 until it runs) -- never
+    reported OK with wrong bytes."""
+    comps = list(malformed["streams"][:300])
+    caps = list(malformed["caps"][:300])
+    want_codes = list(malformed["rc"][:300])
+    outs, st, handed = gu.gpu_decompress_win(torch, comps, caps, dev)
+    for i, (s, code) in enumerate(zip(st, want_codes)):
+        if s == 0:                              # finished: only where the reference says OK
+            assert code == 0 and outs[i] == malformed["outs"][i], (i, code)
+        else:
+            assert s == 0x7FFF0001 and i in handed
+    blocks = [synth.block(synth.ITB, 9100 + i, 65536) for i in range(4)]
+    comps2, _ = gu.gpu_compress(torch, blocks, dev)
+    outs2, st2, handed2 = gu.gpu_decompress_win(torch, comps2, [65535] * 4, dev)
+    assert handed2 == [0, 1, 2, 3] and st2 == [0x7FFF0001] * 4
