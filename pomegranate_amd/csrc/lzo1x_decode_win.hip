@@ -429,11 +429,13 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
                 cur = uni(__builtin_amdgcn_readlane(sx, g - 1));
                 f = g;
             } else {
-                uint32_t w = 0;
+                const uint64_t tw0 = STAMPS ? clock64() : 0;
+                uint32_t w = 0, nwt = 0;
                 if (j == f) {                    // walk from the true entry
                     uint32_t pos = cpos, st = cur & 3u;
                     for (;;) {
                         const Tok t = tok(L, k, pos, st);
+                        nwt++;
                         if (t.fl) {
                             w = pack_pt(k, pos, st);
                             break;
@@ -453,6 +455,10 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
                     x = w;
                 }
                 cur = uni(__builtin_amdgcn_readlane(w, f));
+                if (STAMPS && threadIdx.x == 0) {
+                    L.stamp[13] += clock64() - tw0;
+                    L.stamp[14] += __builtin_amdgcn_readlane(nwt, f);
+                }
                 f++;
             }
         }

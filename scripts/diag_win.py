@@ -48,7 +48,7 @@ for rep in range(2):
 ok = torch.equal(out, src.arena)
 S = stamps.view(nb, 16).cpu().numpy().astype(np.float64)
 names = ["stage", "spec", "settle", "count+scan", "emit", "w_bitmap", "w_ptrs", "w_chase", "w_gather",
-         "windows", "pieces", "chase_rounds", "settle_rounds"]
+         "windows", "pieces", "chase_rounds", "settle_rounds", "settle_walk_cycles", "settle_walk_tokens"]
 tot = S[:, :9].sum(axis=1)
 print({"ok": ok, "fallbacks": int(head[0].item()), "kernel_ms": round(ev0.elapsed_time(ev1), 4),
        "cycles_per_block_mean": round(float(tot.mean())), "cycles_per_block_max": round(float(tot.max()))})
