@@ -629,41 +629,61 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
     const uint32_t excl = wave_incl_scan(lc) - lc;
     const uint32_t obase = iS + before + excl;
 
-    // source pointers; literal bytes go straight into the ring (final)
-    uint32_t e[8];
-    uint32_t lmask = 0, lv0 = 0, lv1 = 0;
+    // source pointers; literal bytes go straight into the ring (final).
+    // Branch-free: every load is issued unconditionally from a clamped address
+    // and the results selected afterwards, so the loads of the 8 bytes share one
+    // wait (a load under a divergent condition becomes a branch with its own
+    // s_waitcnt, and 8 of them serialise).
+    uint32_t e[8], pv[8], sv[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) {
+        uint32_t oi = obase + __builtin_popcount(bits8 & ((2u << i) - 1u));
+        oi = oi < kOpCap ? oi : kOpCap - 1;
+        pv[i] = L.opp[oi];
+        sv[i] = L.ops[oi];
+    }
+    uint32_t lmask = 0, gmask = 0, lv0 = 0, lv1 = 0;
     bool bad = false;
+    uint32_t zv[8];
 #pragma unroll
     for (uint32_t i = 0; i < 8; i++) {
         const uint32_t x = x0 + i;
-        const uint32_t oi = obase + __builtin_popcount(bits8 & ((2u << i) - 1u));
-        uint32_t v = B - x;
-        if (x >= S && x < Ew) {
-            const uint32_t p = L.opp[oi], src = L.ops[oi];
-            if (src & kLitF) {
-                const uint32_t c = (src & kLitG) ? (uint32_t)blk.in[(src & 0xFFFFFFu) + (x - p)]
-                                                 : zbyte(L, (src & 0xFFFFu) + (x - p));
-                lmask |= 1u << i;
-                if (i < 4)
-                    lv0 |= c << (8 * i);
-                else
-                    lv1 |= c << (8 * (i - 4));
-                v = kFin + (x - A);
-            } else {
-                const uint32_t d = src;
-                bad |= d > p;                    // lookbehind (lib/minilzo.c:3628)
-                const uint32_t q0 = p > S ? p : S;
-                const uint32_t kk = x - q0;      // < kW + 16
-                uint32_t qq = (uint32_t)((float)kk * __builtin_amdgcn_rcpf((float)d));
-                int32_t rr = (int32_t)(kk - qq * d);
-                rr += rr < 0 ? (int32_t)d : 0;
-                rr -= rr >= (int32_t)d ? (int32_t)d : 0;
-                const uint32_t t = q0 - d + (uint32_t)rr;
-                bad |= t >= x;                   // (never: keeps every chain strictly backward)
-                v = B - t;
-            }
-        }
-        e[i] = v;
+        const bool valid = x >= S && x < Ew;
+        const bool lit = valid && (sv[i] & kLitF) != 0;
+        lmask |= lit ? 1u << i : 0u;
+        gmask |= lit && (sv[i] & kLitG) ? 1u << i : 0u;
+        const uint32_t zoff = (sv[i] & 0xFFFFu) + (x - pv[i]);        // (garbage unless a zin literal)
+        zv[i] = L.zin[(zoff >> 2) < kZR / 4 ? zoff >> 2 : 0u] >> (8u * (zoff & 3u));
+    }
+    if (__builtin_expect(gmask != 0, 0)) {          // literal runs longer than a piece (HBM)
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++)
+            if ((gmask >> i) & 1u)
+                zv[i] = blk.in[(sv[i] & 0xFFFFFFu) + (x0 + i - pv[i])];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t x = x0 + i;
+        const bool valid = x >= S && x < Ew;
+        const uint32_t p = pv[i], d = sv[i];
+        const uint32_t c = zv[i] & 0xFFu;
+        if (i < 4)
+            lv0 |= ((lmask >> i) & 1u) ? c << (8 * i) : 0u;
+        else
+            lv1 |= ((lmask >> i) & 1u) ? c << (8 * (i - 4)) : 0u;
+        // match: x - d, or for a match of period d < length the last period
+        // before max(op start, window start)
+        const uint32_t q0 = p > S ? p : S;
+        const uint32_t kk = x - q0;                 // < kW + 16
+        const uint32_t dd = d & 0xFFFFu ? d & 0xFFFFu : 1u;
+        const uint32_t qq = (uint32_t)((float)kk * __builtin_amdgcn_rcpf((float)dd));
+        int32_t rr = (int32_t)(kk - qq * dd);
+        rr += rr < 0 ? (int32_t)dd : 0;
+        rr -= rr >= (int32_t)dd ? (int32_t)dd : 0;
+        const uint32_t t = q0 - dd + (uint32_t)rr;
+        const bool match = valid && !((lmask >> i) & 1u);
+        bad |= match && (d > p || t >= x);          // lookbehind (lib/minilzo.c:3628); t >= x never
+        e[i] = !valid ? B - x : ((lmask >> i) & 1u) ? kFin + (x - A) : B - t;
     }
     if (bad)
         L.ctl[C_REFUSE] = 1;
@@ -715,21 +735,19 @@ __device__ bool run_window(WinLds& L, const Blk& blk, uint32_t S, uint32_t Ew, u
             any = false;
             uint32_t w8[8];
 #pragma unroll
-            for (uint32_t i = 0; i < 8; i++) {
+            for (uint32_t i = 0; i < 8; i++) {            // unconditional loads, one wait
                 const uint32_t x = x0 + i;
                 const bool pend = x >= S && x < Ew && e[i] <= T;
                 const uint32_t byteoff = (tabb + 2 * (kW - 1 - (pend ? e[i] : 0u))) & 0xFFFFu;
-                w8[i] = pend ? __hip_atomic_load(&t32[byteoff >> 2], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP) >> (8 * (byteoff & 2))
-                             : 0u;
+                w8[i] = __hip_atomic_load(&t32[byteoff >> 2], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_WORKGROUP) >> (8 * (byteoff & 2));
             }
 #pragma unroll
             for (uint32_t i = 0; i < 8; i++) {
                 const uint32_t x = x0 + i;
-                if (x >= S && x < Ew && e[i] <= T) {
-                    e[i] = w8[i] & 0xFFFFu;
-                    any |= e[i] <= T;
-                }
+                const bool pend = x >= S && x < Ew && e[i] <= T;
+                e[i] = pend ? w8[i] & 0xFFFFu : e[i];
+                any |= pend && e[i] <= T;
             }
             COUNT(11, 1);
 #pragma unroll
