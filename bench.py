@@ -84,6 +84,17 @@ def host_cores():
     return max(1, min(n, cap) if cap > 0 else n)
 
 
+def host_cpu_info():
+    """What `cores` was taken from: the affinity set, the OMP_NUM_THREADS cap
+    and the machine's logical CPUs (a GPU box is a share of a larger machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"affinity_cpus": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "machine_logical_cpus": os.cpu_count()}
+
+
 def _ref_lib():
     """lib/minilzo.c compiled from the reference sources (oracle/_ref), or None."""
     path = os.path.join(ROOT, "oracle", "_ref", "libminilzo_ref.so")
@@ -236,6 +247,7 @@ def cpu_baseline(plain, comps, seconds, roundtrip=True):
     # decompress for the decode-only C2 line; both legs beside it
     rt = 1.0 / (1.0 / res["compress"] + 1.0 / res["decompress"]) if roundtrip else res["decompress"]
     return {"value": round(rt, 4), "unit": "GiB/s", "cores": threads,
+            "host": host_cpu_info(),
             "kind": kind, "compress_value": round(res["compress"], 4),
             "decompress_value": round(res["decompress"], 4),
             "byte_identical_blocks": f"{identical}/{nsample}",
@@ -760,6 +772,37 @@ def run_single(args, lzo, synth):
         out[str(n)] = row
     v = out["65536"]["gpu"]["decompress_us"]
     errors = sum(0 if r.get("exact", True) else 1 for row in out.values() for r in row.values())
+    # concurrent callers (the MDS commit / service threads): 64 KiB calls from
+    # 8 threads at once, combined by the library into shared launches
+    from concurrent.futures import ThreadPoolExecutor
+    n = 65536
+    d = synth.block(synth.ITB, 777 + n, n)
+    nthr, per = 8, max(3, args.steps)
+    bufs = [(ctypes.create_string_buffer(d, n), ctypes.create_string_buffer(n + n // 16 + 128),
+             ctypes.create_string_buffer(n + 64)) for _ in range(nthr)]
+
+    def one(t, what):
+        src, z, back = bufs[t]
+        zl, ol = ulong(0), ulong(0)
+        ok = True
+        lib.lzo1x_1_compress(src, n, z, ctypes.byref(zl), None)
+        for _ in range(per):
+            if what == "compress":
+                ok &= lib.lzo1x_1_compress(src, n, z, ctypes.byref(zl), None) == 0
+            else:
+                ok &= lib.lzo1x_decompress(z, zl.value, back, ctypes.byref(ol), None) == 0 and \
+                    back.raw[:n] == d
+        return ok
+
+    conc = {"threads": nthr, "calls_per_thread": per, "block_bytes": n}
+    for what in ("compress", "decompress"):
+        with ThreadPoolExecutor(nthr) as ex:
+            t0 = time.perf_counter()
+            oks = list(ex.map(lambda t: one(t, what), range(nthr)))
+            dt = time.perf_counter() - t0
+        errors += oks.count(False)
+        conc[f"{what}_calls_per_s"] = round(nthr * per / dt, 1)
+        conc[f"{what}_serial_calls_per_s"] = round(1e6 / out["65536"]["gpu"][f"{what}_us"], 1)
     result = {
         "metric": "LZO1X single-call latency, lzo1x_decompress of one 64 KiB ITB block (us)",
         "value": v, "unit": "us", "n_gpus": 1, "steps": max(3, args.steps), "warmup": 1,
@@ -767,7 +810,7 @@ def run_single(args, lzo, synth):
         "data": "synthetic ITB payload images", "config": {
             "workload": "minilzo.h single calls (host buffers in, host buffers out: H2D, "
                         "kernels, D2H, one stream sync per call) vs lib/minilzo.c on one core"},
-        "calls": out}
+        "calls": out, "concurrent": conc}
     return result, errors
 
 
@@ -806,6 +849,16 @@ def run_others(args, torch, dist, lzo, synth, shard, dev, world, rank, backend):
                      "decode_roofline_frac_rank0": r["roofline"]["frac"], "errors": e}
     except Exception as exc:                       # (reported, never hides the headline)
         out["c4"] = {"error": repr(exc), "errors": 1}
+    if world == 1:
+        # the minilzo.h single calls of the unchanged callers (µs per call)
+        a = copy.copy(args)
+        a.workload, a.steps = "single", 20
+        try:
+            r, e = run_single(a, lzo, synth)
+            out["single"] = {"metric": r["metric"], "calls": r["calls"], "concurrent": r["concurrent"],
+                             "errors": e}
+        except Exception as exc:
+            out["single"] = {"error": repr(exc), "errors": 1}
     return out
 
 

@@ -53,13 +53,20 @@ size_t lzo_mi355x_compress_scratch(uint32_t nblocks);
  * decoder).  The scratch holds a 4-byte-a-block list plus op slots for the
  * workgroups resident at once (not per block): about 100 MB plus 4 bytes a
  * block.  After the call, the u32 at scratch byte 0 counts the blocks the
- * throughput decoder handed to the exact decoder (diagnostic). */
+ * throughput decoder handed to the exact (one wave per block, ~20x slower)
+ * decoder: malformed streams, capacity or look-behind errors, destinations not
+ * 16-byte aligned, empty or >= 16 MiB inputs.  Every valid stream with an
+ * aligned destination stays on the throughput decoder. */
 int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
                               const uint32_t *src_len, uint8_t *dst,
                               const uint64_t *dst_off, const uint32_t *dst_cap,
                               uint32_t *out_len, int32_t *status, uint32_t nblocks,
                               void *scratch, void *stream);
 size_t lzo_mi355x_decompress_scratch(uint32_t nblocks);
+/* The number of blocks the last lzo_mi355x_decompress_dev() on `scratch` handed
+ * to the exact decoder: waits for `stream`, then reads scratch byte 0 into
+ * *count.  Returns 0, or -1 on a copy failure. */
+int lzo_mi355x_decompress_fallbacks(const void *scratch, uint32_t *count, void *stream);
 
 /* Decoded length of each block (the unchecked decoder's view), no output. */
 int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,

@@ -246,9 +246,9 @@ static int use_win_decoder(uint32_t nblocks)
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("POM_DECODER");
-        v = !e ? 2 : strcmp(e, "win") == 0 ? 1 : 0;
+        v = !e ? 3 : strcmp(e, "win") == 0 ? 1 : strcmp(e, "ser") == 0 ? 2 : 0;
     }
-    if (v != 2)
+    if (v != 3)
         return v;
     /* default: the windowed decoder while the batch fits two workgroups per
      * CU (one round; lone blocks decode 1.3-1.5x faster there), the op-set
@@ -305,11 +305,13 @@ static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, cons
     const uint32_t nsets = (uint32_t)scr_sets(nblocks);
     uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nblocks));
     if (win) {
-        /* the windowed decoder: no op sets, only the fallback list */
+        /* the windowed (win == 1) or table-walk (win == 2) decoder: no op
+         * sets, only the fallback list */
         if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
             return -1;
-        if (lzo_mi355x_launch_decompress_win(src, src_off, src_len, dst, dst_off, dst_cap, out_len,
-                                             status, fb, ids, nblocks, s) != 0)
+        if ((win == 2 ? lzo_mi355x_launch_decompress_ser
+                      : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
+                                                          out_len, status, fb, ids, nblocks, s) != 0)
             return -1;
     } else {
         if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)
@@ -334,6 +336,18 @@ int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
 {
     return decompress_dev(src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
                           scratch, 0, (hipStream_t)stream);
+}
+
+int lzo_mi355x_decompress_fallbacks(const void *scratch, uint32_t *count, void *stream)
+{
+    /* the fallback count at scratch byte 0, once the stream has reached it */
+    if (!scratch || !count)
+        return -1;
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemcpyAsync(count, scratch, sizeof *count, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    return 0;
 }
 
 int lzo_mi355x_decoded_length_dev(const uint8_t *src, const uint64_t *src_off,
@@ -876,97 +890,248 @@ const char *lzo_version_string(void) { return LZO_VERSION_STRING; }
 const char *lzo_version_date(void) { return LZO_VERSION_DATE; }
 
 /* ---- single calls ------------------------------------------------------------
- * One block, one stream synchronisation: the header and the input go up, the
- * kernels run, and the header plus an output region the host sizes up front
- * come back in one go.  Staging (device and pinned host alike):
- *   [0, 256)        header: src_off u64, dst_off u64, src_len, dst_cap,
- *                   out_len, status, pre-scan length / status / capacity,
- *                   fallback list (2 words)
- *   [256, +G)       output (G: worst case, the caller's capacity, or a guess)
- *   then the input, then the fast decoder's scratch (device only)
+ * The minilzo.h entry points code one block per call, synchronously.  Calls
+ * that arrive together from several threads on the same GPU (the MDS commit
+ * threads, mds/txg.c:1010-1011, and the service threads that load ITBs,
+ * mds/itb.c:2964) are COMBINED: the first caller becomes the leader and runs
+ * every call queued behind it (of the same kind, up to kScGroup) as one
+ * launch on its own stream; the others sleep until their result is in their
+ * buffer.  A lone call is a group of one.  POM_SC_COMBINE=0 turns combining
+ * off (every call its own launch, as in round 2).
+ * Staging of a group of k calls (device and pinned host alike):
+ *   [0, H)          header arrays: src_off u64[k], dst_off u64[k], src_len[k],
+ *                   dst_cap[k], out_len[k], status[k], pre-scan length[k] and
+ *                   status[k]
+ *   [H, I)          the outputs (each: worst case, the caller's capacity or a
+ *                   guess), 256-byte aligned
+ *   [I, J)          the inputs
+ *   then the decoder's scratch (device only)
  */
-enum { SC_HDR = 256 };
-struct sc_hdr {
-    uint64_t src_off, dst_off;
-    uint32_t src_len, dst_cap, out_len;
-    int32_t status;
-    uint32_t plen;
-    int32_t pstatus;
-    uint32_t pcap;
-    uint32_t fb[2];
-};
+enum { kScGroup = 64 };
+static const size_t kScGroupBytes = (size_t)256 << 20;
 
 enum sc_kind { SC_COMPRESS, SC_SAFE, SC_UNCHECKED };
 
-static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, uint8_t *dst,
-                       size_t room, size_t *produced)
+struct sc_req {
+    enum sc_kind kind;
+    const uint8_t *src;
+    size_t src_len;
+    uint8_t *dst;
+    size_t room;
+    size_t produced;
+    int rc;
+    int done;
+    struct sc_req *next;
+};
+
+struct sc_queue {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    struct sc_req *head, *tail;
+    int leader;
+};
+
+static struct sc_queue sc_q[kMaxDev];
+static pthread_once_t sc_once = PTHREAD_ONCE_INIT;
+
+static void sc_init(void)
 {
+    for (int d = 0; d < kMaxDev; d++) {
+        pthread_mutex_init(&sc_q[d].mu, NULL);
+        pthread_cond_init(&sc_q[d].cv, NULL);
+    }
+}
+
+static int sc_combine(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("POM_SC_COMBINE");
+        v = !(e && strcmp(e, "0") == 0);
+    }
+    return v;
+}
+
+/* header arrays of a group of k */
+struct sc_hdr {
+    uint64_t *src_off, *dst_off;
+    uint32_t *src_len, *dst_cap, *out_len;
+    int32_t *status;
+    uint32_t *plen;
+    int32_t *pstatus;
+};
+
+static size_t sc_hdr_bytes(int k)
+{
+    return ALIGN_UP((size_t)k * 40, 256);
+}
+
+static struct sc_hdr sc_hdr_at(uint8_t *base, int k)
+{
+    struct sc_hdr x;
+    x.src_off = (uint64_t *)base;
+    x.dst_off = x.src_off + k;
+    x.src_len = (uint32_t *)(x.dst_off + k);
+    x.dst_cap = x.src_len + k;
+    x.out_len = x.dst_cap + k;
+    x.status = (int32_t *)(x.out_len + k);
+    x.plen = (uint32_t *)(x.status + k);
+    x.pstatus = (int32_t *)(x.plen + k);
+    return x;
+}
+
+/* One launch for the k calls g[0..k) (all of one kind) on the calling thread's
+ * slot: fills each call's rc and produced length and copies its output. */
+static void sc_run_group(struct sc_req **g, int k)
+{
+    const enum sc_kind kind = g[0]->kind;
+    for (int i = 0; i < k; i++)
+        g[i]->rc = LZO_E_ERROR;
     struct slot *t = single_slot();
-    if (!t || src_len > 0xFFFFFFF0u || room > 0xFFFFFFF0u)
-        return LZO_E_ERROR;
+    if (!t)
+        return;
     const int zc = sc_zero_copy();
-    const size_t o_src = SC_HDR + ALIGN_UP(room, 256);
-    const size_t o_scr = o_src + ALIGN_UP(src_len, 256);
-    const size_t dneed = o_scr + (kind == SC_COMPRESS ? 0 : lzo_mi355x_decompress_scratch(1));
-    if (slot_reserve(t, dneed, o_scr) != 0)
-        return LZO_E_ERROR;
+    const size_t H = sc_hdr_bytes(k);
+    size_t o = H, o_out[kScGroup], o_src[kScGroup];
+    for (int i = 0; i < k; i++) {
+        o_out[i] = o;
+        o += ALIGN_UP(g[i]->room, 256);
+    }
+    const size_t I = o;
+    for (int i = 0; i < k; i++) {
+        o_src[i] = o;
+        o += ALIGN_UP(g[i]->src_len, 256);
+    }
+    const size_t J = o;
+    const size_t dneed = J + (kind == SC_COMPRESS ? 0 : lzo_mi355x_decompress_scratch((uint32_t)k));
+    if (slot_reserve(t, dneed, J) != 0)
+        return;
     uint8_t *h = t->hmem, *d = t->dmem;
     hipStream_t s = t->stream;
-    struct sc_hdr *hh = (struct sc_hdr *)h;
-    memset(hh, 0, sizeof(*hh));
-    hh->src_off = o_src;
-    hh->dst_off = SC_HDR;
-    hh->src_len = (uint32_t)src_len;
-    hh->dst_cap = (uint32_t)room;
-    hh->status = -1;
-    if (src_len)
-        memcpy(h + o_src, src, src_len);
-    struct sc_hdr *dh = (struct sc_hdr *)d;
-    const uint64_t *so = &dh->src_off, *dof = &dh->dst_off;
-    const uint32_t *sl = &dh->src_len;
-    if (hipMemcpyAsync(d, h, sizeof(*hh), hipMemcpyHostToDevice, s) != hipSuccess ||
-        (src_len && hipMemcpyAsync(d + o_src, h + o_src, src_len, hipMemcpyHostToDevice, s) !=
-                        hipSuccess))
-        return LZO_E_ERROR;
-    /* zero copy: output, out_len and status land in the pinned host header/room */
+    struct sc_hdr hh = sc_hdr_at(h, k), dh = sc_hdr_at(d, k);
+    memset(h, 0, H);
+    for (int i = 0; i < k; i++) {
+        hh.src_off[i] = o_src[i];
+        hh.dst_off[i] = o_out[i];
+        hh.src_len[i] = (uint32_t)g[i]->src_len;
+        hh.dst_cap[i] = (uint32_t)g[i]->room;
+        hh.status[i] = -1;
+        if (g[i]->src_len)
+            memcpy(h + o_src[i], g[i]->src, g[i]->src_len);
+    }
+    if (hipMemcpyAsync(d, h, H, hipMemcpyHostToDevice, s) != hipSuccess ||
+        (J > I && hipMemcpyAsync(d + I, h + I, J - I, hipMemcpyHostToDevice, s) != hipSuccess))
+        return;
+    /* zero copy: outputs, out_len and status land in the pinned host staging */
     uint8_t *out = zc ? h : d;
-    uint32_t *olen = zc ? &hh->out_len : &dh->out_len;
-    int32_t *ost = zc ? &hh->status : &dh->status;
-    int rc = 0;
+    uint32_t *olen = zc ? hh.out_len : dh.out_len;
+    int32_t *ost = zc ? hh.status : dh.status;
+    int rc;
     if (kind == SC_COMPRESS) {
-        rc = lzo_mi355x_compress_dev(d, so, sl, out, dof, &dh->dst_cap, olen, ost, 1, NULL,
-                                     s);   /* one block: the LDS dictionary is faster */
+        /* no scratch: the LDS-dictionary encoder, faster for a few blocks */
+        rc = lzo_mi355x_compress_dev(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap, olen, ost,
+                                     (uint32_t)k, NULL, s);
     } else {
         /* SC_UNCHECKED: decoded into the room; the unchecked decoder never
          * reports an output overrun (lib/minilzo.c:3676-3680), so
          * OUTPUT_OVERRUN here means the stream is longer than the room.
          * The windowed decoder never reads its output back (host memory). */
-        rc = decompress_dev_with(d, so, sl, out, dof, &dh->dst_cap, olen, ost, 1, d + o_scr,
-                                 kind == SC_UNCHECKED, 1, s);
+        rc = decompress_dev_with(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap, olen, ost,
+                                 (uint32_t)k, d + J, kind == SC_UNCHECKED, 1, s);
     }
     if (rc != 0 ||
-        (!zc && hipMemcpyAsync(h, d, o_src, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (!zc && (hipMemcpyAsync(h + k * 16, d + k * 16, (size_t)k * 16, hipMemcpyDeviceToHost, s) !=
+                     hipSuccess ||
+                 hipMemcpyAsync(h + H, d + H, I - H, hipMemcpyDeviceToHost, s) != hipSuccess)) ||
         hipStreamSynchronize(s) != hipSuccess)
-        return LZO_E_ERROR;
-    if (kind == SC_UNCHECKED && hh->status == LZO_E_OUTPUT_OVERRUN) {
-        /* rare: the decoded length (input still on the GPU), then the caller
-         * retries with that much room */
-        if (lzo_mi355x_launch_decoded_length(d, so, sl, &dh->plen, &dh->pstatus, 1, NULL,
-                                             0xFFFFFFFFu, s) != 0 ||
-            hipMemcpyAsync(&hh->plen, &dh->plen, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s) !=
-                hipSuccess ||
+        return;
+    int over = 0;
+    for (int i = 0; i < k; i++)
+        over |= kind == SC_UNCHECKED && hh.status[i] == LZO_E_OUTPUT_OVERRUN;
+    if (over) {
+        /* rare: the decoded lengths (inputs still on the GPU); a call whose
+         * stream is longer than its room retries with that much room */
+        if (lzo_mi355x_launch_decoded_length(d, dh.src_off, dh.src_len, dh.plen, dh.pstatus,
+                                             (uint32_t)k, NULL, 0xFFFFFFFFu, s) != 0 ||
+            hipMemcpyAsync(hh.plen, dh.plen, (size_t)k * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
-            return LZO_E_ERROR;
-        if (hh->plen > room) {
-            *produced = hh->plen;
-            return 1;
-        }
+            return;
     }
-    const size_t n = hh->out_len < room ? hh->out_len : room;
-    if (n)
-        memcpy(dst, h + SC_HDR, n);
-    *produced = hh->out_len;
-    return hh->status;
+    for (int i = 0; i < k; i++) {
+        struct sc_req *r = g[i];
+        if (over && hh.status[i] == LZO_E_OUTPUT_OVERRUN && hh.plen[i] > r->room) {
+            r->produced = hh.plen[i];
+            r->rc = 1;
+            continue;
+        }
+        const size_t n = hh.out_len[i] < r->room ? hh.out_len[i] : r->room;
+        if (n)
+            memcpy(r->dst, h + o_out[i], n);
+        r->produced = hh.out_len[i];
+        r->rc = hh.status[i];
+    }
+}
+
+static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, uint8_t *dst,
+                       size_t room, size_t *produced)
+{
+    int dev = 0;
+    if (src_len > 0xFFFFFFF0u || room > 0xFFFFFFF0u || lzo_mi355x_device_count() <= 0 ||
+        hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev)
+        return LZO_E_ERROR;
+    struct sc_req r = {kind, src, src_len, dst, room, 0, LZO_E_ERROR, 0, NULL};
+    if (!sc_combine()) {
+        struct sc_req *g = &r;
+        sc_run_group(&g, 1);
+        *produced = r.produced;
+        return r.rc;
+    }
+    pthread_once(&sc_once, sc_init);
+    struct sc_queue *q = &sc_q[dev];
+    pthread_mutex_lock(&q->mu);
+    if (q->tail)
+        q->tail->next = &r;
+    else
+        q->head = &r;
+    q->tail = &r;
+    while (!r.done) {
+        if (q->leader) {
+            pthread_cond_wait(&q->cv, &q->mu);
+            continue;
+        }
+        /* lead: the queue's oldest calls of the oldest call's kind */
+        q->leader = 1;
+        struct sc_req *g[kScGroup];
+        int k = 0;
+        size_t bytes = 0;
+        const enum sc_kind gk = q->head->kind;
+        struct sc_req **pp = &q->head, *prev = NULL;
+        while (*pp && k < kScGroup) {
+            struct sc_req *x = *pp;
+            const size_t xb = x->room + x->src_len;
+            if (x->kind != gk || (k > 0 && bytes + xb > kScGroupBytes)) {
+                prev = x;
+                pp = &x->next;
+                continue;
+            }
+            *pp = x->next;
+            if (q->tail == x)
+                q->tail = prev;
+            x->next = NULL;
+            g[k++] = x;
+            bytes += xb;
+        }
+        pthread_mutex_unlock(&q->mu);
+        sc_run_group(g, k);
+        pthread_mutex_lock(&q->mu);
+        for (int i = 0; i < k; i++)
+            g[i]->done = 1;
+        q->leader = 0;
+        pthread_cond_broadcast(&q->cv);
+    }
+    pthread_mutex_unlock(&q->mu);
+    *produced = r.produced;
+    return r.rc;
 }
 
 /* lib/minilzo.c:3159-3207.  The output is the reference's with a zero-filled
@@ -1001,25 +1166,25 @@ int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len, unsigne
     struct slot *t = single_slot();
     if (!t || src_len > 0xFFFFFFF0u)
         return LZO_E_ERROR;
-    const size_t o_src = SC_HDR;
+    const size_t o_src = sc_hdr_bytes(1);
     if (slot_reserve(t, o_src + src_len + 16, o_src + src_len + 16) != 0)
         return LZO_E_ERROR;
     uint8_t *h = t->hmem, *d = t->dmem;
     hipStream_t s = t->stream;
-    struct sc_hdr *hh = (struct sc_hdr *)h, *dh = (struct sc_hdr *)d;
-    memset(hh, 0, sizeof(*hh));
-    hh->src_off = o_src;
-    hh->src_len = (uint32_t)src_len;
+    struct sc_hdr hh = sc_hdr_at(h, 1), dh = sc_hdr_at(d, 1);
+    memset(h, 0, o_src);
+    hh.src_off[0] = o_src;
+    hh.src_len[0] = (uint32_t)src_len;
     if (src_len)
         memcpy(h + o_src, src, src_len);
     if (hipMemcpyAsync(d, h, o_src + src_len, hipMemcpyHostToDevice, s) != hipSuccess ||
-        lzo_mi355x_launch_decoded_length(d, &dh->src_off, &dh->src_len, &dh->plen, &dh->pstatus,
-                                         1, NULL, 0xFFFFFFFFu, s) != 0 ||
-        hipMemcpyAsync(h, d, sizeof(*hh), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        lzo_mi355x_launch_decoded_length(d, dh.src_off, dh.src_len, dh.plen, dh.pstatus, 1, NULL,
+                                         0xFFFFFFFFu, s) != 0 ||
+        hipMemcpyAsync(h, d, o_src, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return LZO_E_ERROR;
-    *dst_len = hh->plen;
-    return hh->pstatus;
+    *dst_len = hh.plen[0];
+    return hh.pstatus[0];
 }
 
 /* The unchecked decoder (lib/minilzo.c:3308-3699) that mds/itb.c:2964,

@@ -43,7 +43,7 @@ EXPORTS = (
     "lzo1x_1_compress", "lzo1x_decompress", "lzo1x_decompress_safe",
     "lzo_mi355x_worst_compress", "lzo_mi355x_device_count", "lzo_mi355x_decoded_length",
     "lzo_mi355x_compress_dev", "lzo_mi355x_decompress_dev",
-    "lzo_mi355x_decompress_scratch", "lzo_mi355x_decoded_length_dev",
+    "lzo_mi355x_decompress_scratch", "lzo_mi355x_decompress_fallbacks", "lzo_mi355x_decoded_length_dev",
     "lzo_mi355x_compress_scratch",
     "lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
     "lzo_mi355x_decompress_concat_batch",
@@ -107,6 +107,8 @@ def load() -> ctypes.CDLL:
     lib.lzo_mi355x_decompress_dev.argtypes = dev_args + [_u8p, _u8p]
     lib.lzo_mi355x_decompress_scratch.restype = _size
     lib.lzo_mi355x_decompress_scratch.argtypes = [ctypes.c_uint32]
+    lib.lzo_mi355x_decompress_fallbacks.restype = ctypes.c_int
+    lib.lzo_mi355x_decompress_fallbacks.argtypes = [_u8p, ctypes.POINTER(ctypes.c_uint32), _u8p]
     lib.lzo_mi355x_decoded_length_dev.restype = ctypes.c_int
     lib.lzo_mi355x_decoded_length_dev.argtypes = [_u8p] * 5 + [ctypes.c_uint32, _u8p]
     for name in ("lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
@@ -276,6 +278,18 @@ def decompress_dev(src: DeviceBatch, dst: DeviceBatch, out_len, status, scratch=
         _stream_handle(torch, stream))
     if rc != 0:
         raise RuntimeError("lzo_mi355x_decompress_dev launch failed")
+
+
+def decompress_fallbacks(scratch, stream=None) -> int:
+    """Blocks the last decompress_dev() on `scratch` handed to the exact decoder
+    (waits for `stream`)."""
+    import torch
+    n = ctypes.c_uint32(0)
+    rc = load().lzo_mi355x_decompress_fallbacks(_ptr(scratch), ctypes.byref(n),
+                                                _stream_handle(torch, stream))
+    if rc != 0:
+        raise RuntimeError("lzo_mi355x_decompress_fallbacks failed")
+    return int(n.value)
 
 
 def decompress_scratch_bytes(nblocks: int) -> int:

@@ -1,4 +1,4 @@
-"""A/B of the two throughput decoders on one GPU: the round-2 op-set decoder
+"""A/B of the throughput decoders (fast, win, ser) on one GPU: the round-2 op-set decoder
 (lzo_mi355x_launch_decompress_fast) and the windowed decoder
 (lzo_mi355x_launch_decompress_win), kernel time by HIP events, output checked.
 Workloads: C2 (4096 x 64 KiB ITB), lone blocks (one 64 KiB, one 536,192 B ITB
@@ -25,6 +25,9 @@ fast.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctyp
 win = lib.lzo_mi355x_launch_decompress_win
 win.restype = ctypes.c_int
 win.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
+ser = lib.lzo_mi355x_launch_decompress_ser
+ser.restype = ctypes.c_int
+ser.argtypes = win.argtypes
 lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
 lib.lzo_mi355x_fast_resident_blocks.restype = ctypes.c_uint32
 p = lambda x: x.data_ptr()
@@ -68,7 +71,7 @@ def run(kind, src, za, zb, zl, nb, reps):
             rc = fast(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
                       p(head), p(ids), p(head) + 256, p(ring), p(ops), nsets, nb, s.cuda_stream)
         else:
-            rc = win(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
+            rc = (ser if kind == "ser" else win)(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
                      p(head), p(ids), nb, s.cuda_stream)
         ev1.record(s)
         torch.cuda.synchronize()
@@ -79,6 +82,8 @@ def run(kind, src, za, zb, zl, nb, reps):
     return float(np.median(ts)), ok, fb
 
 
+KINDS = (sys.argv[1] if len(sys.argv) > 1 else "fast,win,ser").split(",")
+ONLY = sys.argv[2].split(",") if len(sys.argv) > 2 else None
 res = {}
 cases = {
     "c2_4096x64k": [65536] * 4096,
@@ -87,10 +92,13 @@ cases = {
     "c5_like_1024": [int(x) for x in np.random.default_rng(3).choice(
         [12416, 40000, 65536, 131072, 262144, 536192], 1024, p=[.3, .2, .2, .15, .1, .05])],
 }
+cases["c4_8192mixed"] = [int(x) for x in synth.mixed_sizes(8192, 5)]
 for name, sizes in cases.items():
+    if ONLY and name not in ONLY:
+        continue
     src, za, zb, zl, nb = setup(sizes, 11)
     n = int(src.length.long().sum())
-    for kind in ("fast", "win"):
+    for kind in KINDS:
         ms, ok, fb = run(kind, src, za, zb, zl, nb, 5)
         res[f"{name}/{kind}"] = {"ms": round(ms, 4), "gibps": round(n / (ms / 1e3) / 2**30, 2), "ok": ok,
                                  "fallbacks": fb}

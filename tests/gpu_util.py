@@ -91,12 +91,14 @@ def fetch(batch, olen, cap=None) -> List[bytes]:
     return res
 
 
-def gpu_decompress_win(torch, comps: Sequence[bytes], caps: Sequence[int], dev):
-    """The windowed decoder alone (lzo_mi355x_launch_decompress_win): outputs,
-    statuses and the ids of the blocks it handed over (fallback list)."""
+def gpu_decompress_win(torch, comps: Sequence[bytes], caps: Sequence[int], dev, kind: str = "win"):
+    """One throughput decoder alone, without the exact decoder behind it: the
+    windowed one (kind "win", lzo_mi355x_launch_decompress_win) or the
+    table-walk one ("ser", lzo_mi355x_launch_decompress_ser).  Returns the
+    outputs, statuses and the ids of the blocks it handed over (fallback list)."""
     import ctypes
     lib = lzo.load()
-    fn = lib.lzo_mi355x_launch_decompress_win
+    fn = getattr(lib, f"lzo_mi355x_launch_decompress_{kind}")
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
     src = device_batch(torch, comps, dev)

@@ -140,6 +140,36 @@ def test_unchecked_decompress_codes(dev, unchecked):
     assert not bad, bad[:8]
 
 
+def test_single_calls_from_many_threads(dev, oracle):
+    """Single calls arriving together from several threads (the MDS commit and
+    service threads, mds/txg.c:1010-1011, mds/itb.c:2964) are combined into
+    shared launches (lzo_host.c single_call); every caller still gets exactly
+    its own bytes, length and return code, whatever else shares its launch."""
+    from concurrent.futures import ThreadPoolExecutor
+    sizes = [12416, 65536, 100, 300000, 4096, 1, 70000, 536192] * 4
+    blocks = [synth.block(synth.ITB if i % 3 else synth.TEXT, 4242 + i, n) for i, n in enumerate(sizes)]
+    want = [oracle.compress(b) for b in blocks]
+
+    def work(i):
+        d, z = blocks[i], want[i]
+        out = []
+        for _ in range(3):
+            rc, got = lzo.lzo1x_1_compress(d)
+            out.append(rc == 0 and got == z)
+            rc, back = lzo.lzo1x_decompress(z)
+            out.append(rc == 0 and back == d)
+            rc, back = lzo.lzo1x_decompress_safe(z, len(d))
+            out.append(rc == 0 and back == d)
+            rc, _ = lzo.lzo1x_decompress_safe(z, len(d) - 1)      # one byte short
+            out.append(rc == lzo.LZO_E_OUTPUT_OVERRUN)
+        return i, out
+
+    with ThreadPoolExecutor(8) as ex:
+        res = list(ex.map(work, range(len(blocks))))
+    bad = [(i, o) for i, o in res if not all(o)]
+    assert not bad, bad[:4]
+
+
 @pytest.mark.parametrize("n", [65536, 262145, 536192, (2 << 20) + 7])
 def test_unchecked_single_call_large_output(dev, oracle, n):
     """Outputs beyond the single call's first guess (16x the input, at least
@@ -612,9 +642,10 @@ def test_encoder_block_tickets_mixed_sizes(dev, gu):
     assert torch.equal(back, src.arena)
 
 
-def test_window_decoder_every_valid_stream(dev, gu):
-    """The windowed decoder (lzo1x_decode_win.hip) alone, without the exact
-    decoder behind it: every content model (incompressible blocks with
+@pytest.mark.parametrize("kind", ["win", "ser"])
+def test_window_decoder_every_valid_stream(dev, gu, kind):
+    """The windowed (lzo1x_decode_win.hip) and table-walk
+    (lzo1x_decode_ser.hip) decoders alone, without the exact decoder behind it: every content model (incompressible blocks with
     literal runs far longer than a 2 KiB piece, all-zero blocks with length
     extensions past a piece), ITB blocks over the C4/C5 size range, the
     adversarial blocks and a 1 MiB block (the 64 KiB LDS ring wraps 16 times)
@@ -630,14 +661,15 @@ def test_window_decoder_every_valid_stream(dev, gu):
     blocks.append(synth.block(synth.LZLIKE, 77, 1 << 20))
     comps, st = gu.gpu_compress(torch, blocks, dev)
     assert all(s == 0 for s in st)
-    outs, st2, handed = gu.gpu_decompress_win(torch, comps, [len(b) for b in blocks], dev)
+    outs, st2, handed = gu.gpu_decompress_win(torch, comps, [len(b) for b in blocks], dev, kind)
     assert handed == []
     assert st2 == [0] * len(blocks)
     bad = [i for i, (o, b) in enumerate(zip(outs, blocks)) if o != b]
     assert not bad, bad[:8]
 
 
-def test_window_decoder_full_grammar_streams(dev, gu):
+@pytest.mark.parametrize("kind", ["win", "ser"])
+def test_window_decoder_full_grammar_streams(dev, gu, kind):
     """LZO1X streams the LZO1X-1 compressor never writes (M1 after literal runs
     and trailing literals, long extensions, first runs of 1-3 bytes) decode
     bit-exactly on the windowed decoder, none handed over."""
@@ -646,20 +678,21 @@ def test_window_decoder_full_grammar_streams(dev, gu):
                for s in range(80)]
     comps = [z for z, _ in streams]
     want = [o for _, o in streams]
-    outs, st, handed = gu.gpu_decompress_win(torch, comps, [len(o) for o in want], dev)
+    outs, st, handed = gu.gpu_decompress_win(torch, comps, [len(o) for o in want], dev, kind)
     assert handed == []
     assert st == [0] * len(want)
     assert outs == want
 
 
-def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, malformed):
+@pytest.mark.parametrize("kind", ["win", "ser"])
+def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, kind, malformed):
     """Malformed streams, and valid streams whose output does not fit, are
     handed to the exact decoder (status 0x7FFF0001 until it runs) -- never
     reported OK with wrong bytes."""
     comps = list(malformed["streams"][:300])
     caps = list(malformed["caps"][:300])
     want_codes = list(malformed["rc"][:300])
-    outs, st, handed = gu.gpu_decompress_win(torch, comps, caps, dev)
+    outs, st, handed = gu.gpu_decompress_win(torch, comps, caps, dev, kind)
     for i, (s, code) in enumerate(zip(st, want_codes)):
         if s == 0:                              # finished: only where the reference says OK
             assert code == 0 and outs[i] == malformed["outs"][i], (i, code)
@@ -667,5 +700,5 @@ def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, malformed):
             assert s == 0x7FFF0001 and i in handed
     blocks = [synth.block(synth.ITB, 9100 + i, 65536) for i in range(4)]
     comps2, _ = gu.gpu_compress(torch, blocks, dev)
-    outs2, st2, handed2 = gu.gpu_decompress_win(torch, comps2, [65535] * 4, dev)
+    outs2, st2, handed2 = gu.gpu_decompress_win(torch, comps2, [65535] * 4, dev, kind)
     assert handed2 == [0, 1, 2, 3] and st2 == [0x7FFF0001] * 4
