@@ -150,22 +150,31 @@ static struct dctx *dctx_get(struct tctx *t, int device)
 
 static int slot_reserve(struct slot *t, size_t dbytes, size_t hbytes)
 {
+    /* growth: +25%, or doubling up to 64 MiB (combined single calls grow
+     * their groups step by step; each regrowth is a hipMalloc/hipHostMalloc) */
+    const size_t kDoubleMax = (size_t)64 << 20;
     if (dbytes > t->dcap) {
+        const size_t old = t->dcap;
         if (t->dmem)
             hipFree(t->dmem);
         t->dmem = NULL;
         t->dcap = 0;
         size_t want = ALIGN_UP(dbytes + dbytes / 4, 1 << 20);
+        if (want < 2 * old && 2 * old <= kDoubleMax)
+            want = 2 * old;
         if (hipMalloc((void **)&t->dmem, want) != hipSuccess)
             return -1;
         t->dcap = want;
     }
     if (hbytes > t->hcap) {
+        const size_t old = t->hcap;
         if (t->hmem)
             hipHostFree(t->hmem);
         t->hmem = NULL;
         t->hcap = 0;
         size_t want = ALIGN_UP(hbytes + hbytes / 4, 1 << 20);
+        if (want < 2 * old && 2 * old <= kDoubleMax)
+            want = 2 * old;
         if (hipHostMalloc((void **)&t->hmem, want, hipHostMallocDefault) != hipSuccess)
             return -1;
         t->hcap = want;
@@ -929,6 +938,9 @@ struct sc_queue {
     pthread_cond_t cv;
     struct sc_req *head, *tail;
     int leader;
+    int last_k;                 /* size of the last group (a hint that callers come together) */
+    int ready;                  /* slot and stream below created */
+    struct slot slot;           /* the groups' staging: one leader at a time per device */
 };
 
 static struct sc_queue sc_q[kMaxDev];
@@ -982,12 +994,32 @@ static struct sc_hdr sc_hdr_at(uint8_t *base, int k)
 
 /* One launch for the k calls g[0..k) (all of one kind) on the calling thread's
  * slot: fills each call's rc and produced length and copies its output. */
-static void sc_run_group(struct sc_req **g, int k)
+/* The staging of combined groups on the calling thread's device: the leader
+ * flag gives one group at a time per device, so one slot serves every thread
+ * (per-thread slots each grew to the groups their thread happened to lead,
+ * and every regrowth is a hipMalloc / hipHostMalloc). */
+static struct slot *sc_slot(struct sc_queue *q)
+{
+    if (!q)
+        return single_slot();
+    if (!q->ready) {
+        if (hipStreamCreateWithFlags(&q->slot.stream, hipStreamNonBlocking) != hipSuccess)
+            return NULL;
+        q->ready = 1;
+    }
+    return &q->slot;
+}
+
+static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
 {
     const enum sc_kind kind = g[0]->kind;
+    static int trace = -1;
+    if (trace < 0)
+        trace = getenv("POM_SC_TRACE") != NULL;
+    const double t0 = trace ? now_ms() : 0.0;
     for (int i = 0; i < k; i++)
         g[i]->rc = LZO_E_ERROR;
-    struct slot *t = single_slot();
+    struct slot *t = sc_slot(q);
     if (!t)
         return;
     const int zc = sc_zero_copy();
@@ -1070,6 +1102,8 @@ static void sc_run_group(struct sc_req **g, int k)
         r->produced = hh.out_len[i];
         r->rc = hh.status[i];
     }
+    if (trace)
+        fprintf(stderr, "pom single-call group: kind %d, %d calls, %.3f ms\n", (int)kind, k, now_ms() - t0);
 }
 
 static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, uint8_t *dst,
@@ -1082,7 +1116,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
     struct sc_req r = {kind, src, src_len, dst, room, 0, LZO_E_ERROR, 0, NULL};
     if (!sc_combine()) {
         struct sc_req *g = &r;
-        sc_run_group(&g, 1);
+        sc_run_group(&g, 1, NULL);
         *produced = r.produced;
         return r.rc;
     }
@@ -1094,13 +1128,27 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
     else
         q->head = &r;
     q->tail = &r;
+    if (q->leader)
+        pthread_cond_broadcast(&q->cv);         /* (a leader may be waiting for company) */
     while (!r.done) {
         if (q->leader) {
             pthread_cond_wait(&q->cv, &q->mu);
             continue;
         }
-        /* lead: the queue's oldest calls of the oldest call's kind */
+        /* lead: the queue's oldest calls of the oldest call's kind.  When the
+         * last group had company and this one would not, the other callers
+         * are probably between two calls: give them ~50 us to queue */
         q->leader = 1;
+        if (q->last_k > 1 && q->head == q->tail) {
+            struct timespec ts;
+            clock_gettime(CLOCK_REALTIME, &ts);
+            ts.tv_nsec += 50000;
+            if (ts.tv_nsec >= 1000000000L) {
+                ts.tv_sec++;
+                ts.tv_nsec -= 1000000000L;
+            }
+            pthread_cond_timedwait(&q->cv, &q->mu, &ts);
+        }
         struct sc_req *g[kScGroup];
         int k = 0;
         size_t bytes = 0;
@@ -1122,11 +1170,12 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
             bytes += xb;
         }
         pthread_mutex_unlock(&q->mu);
-        sc_run_group(g, k);
+        sc_run_group(g, k, q);
         pthread_mutex_lock(&q->mu);
         for (int i = 0; i < k; i++)
             g[i]->done = 1;
         q->leader = 0;
+        q->last_k = k;
         pthread_cond_broadcast(&q->cv);
     }
     pthread_mutex_unlock(&q->mu);

@@ -54,11 +54,13 @@ def run(sizes):
         assert rc == 0
     ok = int(head[0].item()) == 0 and torch.equal(out, src.arena)
     a = stamps.view(nb, 16).cpu().numpy().astype(np.float64).mean(axis=0)
-    tot = a[:8].sum()
+    tot = a[:8].sum()          # (the walker's phases 0-1 overlap the executor's 2-7)
     print(f"blocks {nb}: kernel {ev0.elapsed_time(ev1):.3f} ms, exact {ok}, cycles/block {tot:.0f}")
     for i, nm in enumerate(NAMES):
         print(f"  {nm:12s} {a[i]:10.0f}  {100 * a[i] / tot:5.1f}%")
     print("  windows %.1f  instructions %.1f  slow near %.1f  far %.1f  slow lits %.1f" % tuple(a[8:13]))
+    print("  executor barrier waits %.0f cycles/block (walker: stage+table+walk %.0f; executor phases 2-7 %.0f)"
+          % (a[13], a[0] + a[1], a[2:8].sum()))
 
 
 run([65536])

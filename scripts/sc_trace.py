@@ -1,0 +1,42 @@
+"""Combined single calls: 8 threads of 64 KiB lzo1x_1_compress / lzo1x_decompress
+calls at once; run with POM_SC_TRACE=1 to see the group sizes the library forms."""
+import ctypes
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from pomegranate_amd import lzo, synth  # noqa: E402
+
+lib = lzo.load()
+n = 65536
+d = synth.block(synth.ITB, 777 + n, n)
+zbuf = ctypes.create_string_buffer(n + n // 16 + 128)
+zl = ctypes.c_ulong(0)
+lib.lzo1x_1_compress(d, n, zbuf, ctypes.byref(zl), None)
+z = zbuf.raw[: zl.value]
+
+
+def work(what, per):
+    back = ctypes.create_string_buffer(n + 64)
+    out = ctypes.create_string_buffer(n + n // 16 + 128)
+    ol = ctypes.c_ulong(0)
+    for _ in range(per):
+        if what == "d":
+            assert lib.lzo1x_decompress(z, len(z), back, ctypes.byref(ol), None) == 0
+        else:
+            assert lib.lzo1x_1_compress(d, n, out, ctypes.byref(ol), None) == 0
+
+
+for what in ("c", "d"):
+    for thr in (1, 8):
+        with ThreadPoolExecutor(thr) as ex:
+            list(ex.map(lambda _: work(what, 3), range(thr)))
+        print(f"---- {what} x{thr}", file=sys.stderr, flush=True)
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(thr) as ex:
+            list(ex.map(lambda _: work(what, 10), range(thr)))
+        dt = time.perf_counter() - t0
+        print(what, thr, f"{thr * 10 / dt:.0f} calls/s", flush=True)
