@@ -82,26 +82,65 @@ static struct pom_xnet_tx header(uint8_t type, uint16_t flag, uint64_t ssite, ui
     return tx;
 }
 
+/* Headers of n messages with data[b] (len[b] bytes) laid out back to back in
+ * `wire`: headers written here, the data copied by pom_copy_parallel (threads
+ * once the batch is large).  *wire_len = the bytes of the messages that fit;
+ * -ENOSPC when not all of them did, LZO_E_OUT_OF_MEMORY without scratch. */
+static int frame_batch(const struct pom_xnet_tx *tx, const uint8_t *const *data, const uint32_t *len,
+                       size_t n, uint8_t *wire, size_t cap, size_t *wire_len)
+{
+    uint8_t **dp = malloc(n * sizeof(*dp));
+    size_t *ln = malloc(n * sizeof(*ln));
+    if (!dp || !ln) {
+        free(dp);
+        free(ln);
+        return LZO_E_OUT_OF_MEMORY;
+    }
+    size_t off = 0, k = 0;
+    int rc = 0;
+    for (; k < n; k++) {
+        const size_t need = POM_XNET_TX_SIZE + (size_t)len[k];
+        if (cap - off < need) {
+            rc = -ENOSPC;
+            break;
+        }
+        struct pom_xnet_tx t = tx[k];
+        t.len = len[k];
+        memcpy(wire + off, &t, POM_XNET_TX_SIZE);
+        dp[k] = wire + off + POM_XNET_TX_SIZE;
+        ln[k] = len[k];
+        off += need;
+    }
+    pom_copy_parallel(dp, data, ln, k);
+    *wire_len = off;
+    free(dp);
+    free(ln);
+    return rc;
+}
+
 int pom_xnet_itb_reply_batch(const uint8_t *const *itb, const struct pom_xnet_req *req, size_t n,
                              uint64_t site_id, uint8_t magic, uint8_t *wire, size_t cap,
                              size_t *wire_len)
 {
-    size_t off = 0;
     *wire_len = 0;
-    for (size_t b = 0; b < n; b++) {
-        struct pom_xnet_tx tx = header(POM_XNET_MSG_RPY, POM_XNET_NEED_DATA_FREE, site_id,
-                                       req[b].ssite_id, magic);
-        tx.reqno = req[b].reqno;                    /* xnet_msg_fill_reqno */
-        tx.cmd = POM_XNET_RPY_DATA_ITB;             /* xnet_msg_fill_cmd(rpy, ..., 0, 0) */
-        tx.handle = req[b].handle;                  /* match the request at its source */
-        const size_t w = pom_xnet_frame(wire + off, cap - off, &tx, itb[b],
-                                        rd32(itb[b] + POM_ITBH_LEN_OFF));
-        if (!w)
-            return -ENOSPC;
-        off += w;
-        *wire_len = off;
+    if (n == 0)
+        return 0;
+    struct pom_xnet_tx *tx = malloc(n * sizeof(*tx));
+    uint32_t *len = malloc(n * sizeof(*len));
+    int rc = LZO_E_OUT_OF_MEMORY;
+    if (tx && len) {
+        for (size_t b = 0; b < n; b++) {
+            tx[b] = header(POM_XNET_MSG_RPY, POM_XNET_NEED_DATA_FREE, site_id, req[b].ssite_id, magic);
+            tx[b].reqno = req[b].reqno;             /* xnet_msg_fill_reqno */
+            tx[b].cmd = POM_XNET_RPY_DATA_ITB;      /* xnet_msg_fill_cmd(rpy, ..., 0, 0) */
+            tx[b].handle = req[b].handle;           /* match the request at its source */
+            len[b] = rd32(itb[b] + POM_ITBH_LEN_OFF);
+        }
+        rc = frame_batch(tx, itb, len, n, wire, cap, wire_len);
     }
-    return 0;
+    free(tx);
+    free(len);
+    return rc;
 }
 
 int pom_xnet_itb_wb_batch(uint8_t *const *itb, uint8_t *const *tmp, const size_t *tmp_cap,
@@ -112,29 +151,29 @@ int pom_xnet_itb_wb_batch(uint8_t *const *itb, uint8_t *const *tmp, const size_t
     if (n == 0)
         return 0;
     uint8_t **oi = malloc(n * sizeof(*oi));
-    if (!oi)
-        return LZO_E_OUT_OF_MEMORY;
-    int rc = pom_itb_lzo_compress_batch(itb, tmp, tmp_cap, oi, err, n);
-    if (rc == LZO_E_OK) {
-        size_t off = 0;
-        for (size_t b = 0; b < n; b++) {
-            const uint8_t *rec = err[b] ? itb[b] : oi[b];
-            struct pom_xnet_tx tx = header(POM_XNET_MSG_REQ, 0, site_id, wb[b].dsite_id, magic);
-            tx.cmd = POM_HVFS_MDS2MDSL_WBTXG;       /* xnet_msg_fill_cmd(msg, WBTXG, ITB, txg) */
-            tx.arg0 = POM_HVFS_WBTXG_ITB;
-            tx.arg1 = txg;
-            tx.reserved = wb[b].vid;
-            const size_t w = pom_xnet_frame(wire + off, cap - off, &tx, rec,
-                                            rd32(rec + POM_ITBH_LEN_OFF));
-            if (!w) {
-                rc = -ENOSPC;
-                break;
+    struct pom_xnet_tx *tx = malloc(n * sizeof(*tx));
+    uint32_t *len = malloc(n * sizeof(*len));
+    const uint8_t **rec = malloc(n * sizeof(*rec));
+    int rc = LZO_E_OUT_OF_MEMORY;
+    if (oi && tx && len && rec) {
+        rc = pom_itb_lzo_compress_batch(itb, tmp, tmp_cap, oi, err, n);
+        if (rc == LZO_E_OK) {
+            for (size_t b = 0; b < n; b++) {
+                rec[b] = err[b] ? itb[b] : oi[b];
+                tx[b] = header(POM_XNET_MSG_REQ, 0, site_id, wb[b].dsite_id, magic);
+                tx[b].cmd = POM_HVFS_MDS2MDSL_WBTXG;    /* xnet_msg_fill_cmd(msg, WBTXG, ITB, txg) */
+                tx[b].arg0 = POM_HVFS_WBTXG_ITB;
+                tx[b].arg1 = txg;
+                tx[b].reserved = wb[b].vid;
+                len[b] = rd32(rec[b] + POM_ITBH_LEN_OFF);
             }
-            off += w;
-            *wire_len = off;
+            rc = frame_batch(tx, rec, len, n, wire, cap, wire_len);
         }
     }
     free(oi);
+    free(tx);
+    free(len);
+    free(rec);
     return rc;
 }
 
