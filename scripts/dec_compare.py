@@ -31,6 +31,7 @@ ser.argtypes = win.argtypes
 lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
 lib.lzo_mi355x_fast_resident_blocks.restype = ctypes.c_uint32
 p = lambda x: x.data_ptr()
+mix_streams = (torch.cuda.Stream(), torch.cuda.Stream())
 
 
 def setup(sizes, seed):
@@ -60,14 +61,32 @@ def run(kind, src, za, zb, zl, nb, reps):
     ops = torch.empty(max(nsets, 1) * lib.lzo_mi355x_fast_ops_bytes_per_block(), dtype=torch.uint8,
                       device=dev)
     s = torch.cuda.current_stream()
+    head2 = torch.zeros(64, dtype=torch.int32, device=dev)
+    ids2 = torch.zeros(nb, dtype=torch.int32, device=dev)
     ts = []
     for _ in range(reps):
         head.zero_()
+        head2.zero_()
         ring.zero_()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record(s)
-        if kind == "fast":
+        if kind.startswith("mix"):
+            # blocks [0, nf) on the op-set decoder, [nf, nb) on the table-walk
+            # decoder, on two streams at once: their workgroups share the CUs
+            # (op-set: SALU-heavy; table-walk: VALU-heavy)
+            nf = nb * (100 - int(kind[3:])) // 100
+            s1, s2 = mix_streams
+            s1.wait_stream(s)
+            s2.wait_stream(s)
+            rc = fast(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
+                      p(head), p(ids), p(head) + 256, p(ring), p(ops), nsets, nf, s1.cuda_stream)
+            rc |= ser(p(za), p(zb.off) + 8 * nf, p(zl) + 4 * nf, p(out), p(src.off) + 8 * nf,
+                      p(src.length) + 4 * nf, p(ol) + 4 * nf, p(st) + 4 * nf, p(head2), p(ids2),
+                      nb - nf, s2.cuda_stream)
+            s.wait_stream(s1)
+            s.wait_stream(s2)
+        elif kind == "fast":
             rc = fast(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
                       p(head), p(ids), p(head) + 256, p(ring), p(ops), nsets, nb, s.cuda_stream)
         else:
@@ -77,7 +96,7 @@ def run(kind, src, za, zb, zl, nb, reps):
         torch.cuda.synchronize()
         assert rc == 0
         ts.append(ev0.elapsed_time(ev1))
-    fb = int(head[0].item())
+    fb = int(head[0].item()) + int(head2[0].item())
     ok = fb == 0 and torch.equal(out, src.arena)
     return float(np.median(ts)), ok, fb
 
