@@ -1,28 +1,32 @@
 // lzo1x_decode_ser.hip -- the table-walk LZO1X decoder for MI355X (gfx950):
-// one wave per block, 16-17 blocks per CU, nothing shared between waves.
+// one workgroup of two waves per block, 16 blocks per CU.
 //
 // The block's compressed stream is taken in WINDOWS of at most 256 bytes and
 // 64 instructions (lib/minilzo.c:3308-3699 is the grammar, SURVEY.md Appendix
-// A.2):
+// A.2).  The WALKER wave (wave 1) prepares window i while the EXECUTOR wave
+// (wave 0) runs window i - 1; one barrier per window hands the slot over.
 //
-//  1. STAGE: the window's 512 input bytes into LDS (one dwordx2 per lane).
+// Walker:
+//  1. STAGE: the window's 384 input bytes into LDS (one dwordx2 per lane).
 //  2. TABLE: every lane decodes the instructions that would start at its 4
 //     positions, once as state A (top of the loop: t < 16 is a literal run)
 //     and once as state B/C (after literals: t < 16 is an M1 match), into one
 //     byte each: the instruction's length including its trailing literals and
 //     the state after it.  Rare instructions (a zero length-extension byte,
-//     literal runs over 61 bytes, EOF) get 0, "decode slowly".
+//     literal runs over 61 bytes, EOF, the first byte) get 0, "decode slowly".
 //  3. WALK: from the window's first instruction start the wave follows the
-//     table, one LDS read per instruction, and lane k keeps the k-th start.
-//  4. DECODE: lane k decodes its instruction (match length, distance,
-//     literal count and source); an exclusive scan gives every instruction's
-//     output position, and the capacity / look-behind checks are lane-parallel.
+//     table, one LDS read per instruction; the list of starts goes to LDS.
+// Executor:
+//  4. DECODE: lane k decodes instruction k (match length, distance, literal
+//     count and source); an inclusive scan gives every instruction's output
+//     position, and the capacity / look-behind checks are lane-parallel.
 //  5. EXECUTE: one pass per instruction in order.  A pass moves up to 64
 //     bytes, one per lane, into an 8 KiB LDS output ring: match bytes from
-//     the ring (a period-d match reads byte l mod d of its period), trailing
-//     literal bytes from the staged input, in the same ds_read_u8.  Long
-//     matches, matches from more than 8 KiB back (read from the block's own
-//     output in HBM) and long literal runs take a pass loop.
+//     the ring (a period-d match reads byte l mod d of its period) or from a
+//     far-source slot read at the window's start (more than 8 KiB back),
+//     trailing literal bytes from the staged input, in the same ds_read_u8.
+//     Long matches, further far sources and long literal runs take a pass
+//     loop.
 //  6. FLUSH: completed 1 KiB pieces of the ring go to HBM, one dwordx4 store
 //     per lane.
 //
