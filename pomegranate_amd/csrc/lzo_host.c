@@ -910,11 +910,13 @@ const char *lzo_version_date(void) { return LZO_VERSION_DATE; }
  * Staging of a group of k calls (device and pinned host alike):
  *   [0, H)          header arrays: src_off u64[k], dst_off u64[k], src_len[k],
  *                   dst_cap[k], out_len[k], status[k], pre-scan length[k] and
- *                   status[k]
- *   [H, I)          the outputs (each: worst case, the caller's capacity or a
- *                   guess), 256-byte aligned
- *   [I, J)          the inputs
- *   then the decoder's scratch (device only)
+ *                   status[k], the decoder's fallback list (count + k ids)
+ *   [H, I)          the inputs, 256-byte aligned
+ *   [I, J)          the outputs (each: worst case, the caller's capacity or a
+ *                   guess); with zero copy they are written to the host side only
+ * One H2D copy ([0, I)), one kernel, one synchronisation: the windowed decoder
+ * refuses few valid streams, so the exact decoder runs only when a status says
+ * a block was handed over.
  */
 enum { kScGroup = 64 };
 static const size_t kScGroupBytes = (size_t)256 << 20;
@@ -971,11 +973,12 @@ struct sc_hdr {
     int32_t *status;
     uint32_t *plen;
     int32_t *pstatus;
+    uint32_t *fb;               /* the decoder's fallback list: count, then k ids */
 };
 
 static size_t sc_hdr_bytes(int k)
 {
-    return ALIGN_UP((size_t)k * 40, 256);
+    return ALIGN_UP((size_t)k * 44 + 4, 256);
 }
 
 static struct sc_hdr sc_hdr_at(uint8_t *base, int k)
@@ -989,6 +992,7 @@ static struct sc_hdr sc_hdr_at(uint8_t *base, int k)
     x.status = (int32_t *)(x.out_len + k);
     x.plen = (uint32_t *)(x.status + k);
     x.pstatus = (int32_t *)(x.plen + k);
+    x.fb = (uint32_t *)(x.pstatus + k);
     return x;
 }
 
@@ -1026,17 +1030,16 @@ static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
     const size_t H = sc_hdr_bytes(k);
     size_t o = H, o_out[kScGroup], o_src[kScGroup];
     for (int i = 0; i < k; i++) {
-        o_out[i] = o;
-        o += ALIGN_UP(g[i]->room, 256);
-    }
-    const size_t I = o;
-    for (int i = 0; i < k; i++) {
         o_src[i] = o;
         o += ALIGN_UP(g[i]->src_len, 256);
     }
+    const size_t I = o;
+    for (int i = 0; i < k; i++) {
+        o_out[i] = o;
+        o += ALIGN_UP(g[i]->room, 256);
+    }
     const size_t J = o;
-    const size_t dneed = J + (kind == SC_COMPRESS ? 0 : lzo_mi355x_decompress_scratch((uint32_t)k));
-    if (slot_reserve(t, dneed, J) != 0)
+    if (slot_reserve(t, J, J) != 0)
         return;
     uint8_t *h = t->hmem, *d = t->dmem;
     hipStream_t s = t->stream;
@@ -1051,8 +1054,7 @@ static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
         if (g[i]->src_len)
             memcpy(h + o_src[i], g[i]->src, g[i]->src_len);
     }
-    if (hipMemcpyAsync(d, h, H, hipMemcpyHostToDevice, s) != hipSuccess ||
-        (J > I && hipMemcpyAsync(d + I, h + I, J - I, hipMemcpyHostToDevice, s) != hipSuccess))
+    if (hipMemcpyAsync(d, h, I, hipMemcpyHostToDevice, s) != hipSuccess)
         return;
     /* zero copy: outputs, out_len and status land in the pinned host staging */
     uint8_t *out = zc ? h : d;
@@ -1067,16 +1069,32 @@ static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
         /* SC_UNCHECKED: decoded into the room; the unchecked decoder never
          * reports an output overrun (lib/minilzo.c:3676-3680), so
          * OUTPUT_OVERRUN here means the stream is longer than the room.
-         * The windowed decoder never reads its output back (host memory). */
-        rc = decompress_dev_with(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap, olen, ost,
-                                 (uint32_t)k, d + J, kind == SC_UNCHECKED, 1, s);
+         * The windowed decoder never reads its output back (host memory);
+         * its fallback list lives in the header (zeroed by the H2D copy). */
+        rc = lzo_mi355x_launch_decompress_win(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap,
+                                              olen, ost, dh.fb, dh.fb + 1, (uint32_t)k, s);
     }
+    /* (copy mode: lengths and statuses, then the outputs) */
     if (rc != 0 ||
         (!zc && (hipMemcpyAsync(h + k * 16, d + k * 16, (size_t)k * 16, hipMemcpyDeviceToHost, s) !=
                      hipSuccess ||
-                 hipMemcpyAsync(h + H, d + H, I - H, hipMemcpyDeviceToHost, s) != hipSuccess)) ||
+                 hipMemcpyAsync(h + I, d + I, J - I, hipMemcpyDeviceToHost, s) != hipSuccess)) ||
         hipStreamSynchronize(s) != hipSuccess)
         return;
+    if (kind != SC_COMPRESS) {
+        int handed = 0;
+        for (int i = 0; i < k; i++)
+            handed |= hh.status[i] == 0x7FFF0001;       /* (the throughput decoders' "exact decoder pending") */
+        if (handed &&
+            (lzo_mi355x_launch_decompress_exact(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap,
+                                                olen, ost, dh.fb, dh.fb + 1, (uint32_t)k, (uint32_t)k,
+                                                kind == SC_UNCHECKED, s) != 0 ||
+             (!zc && (hipMemcpyAsync(h + k * 16, d + k * 16, (size_t)k * 16, hipMemcpyDeviceToHost, s) !=
+                          hipSuccess ||
+                      hipMemcpyAsync(h + I, d + I, J - I, hipMemcpyDeviceToHost, s) != hipSuccess)) ||
+             hipStreamSynchronize(s) != hipSuccess))
+            return;
+    }
     int over = 0;
     for (int i = 0; i < k; i++)
         over |= kind == SC_UNCHECKED && hh.status[i] == LZO_E_OUTPUT_OVERRUN;
