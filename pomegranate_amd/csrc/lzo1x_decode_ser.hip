@@ -94,6 +94,7 @@ struct Src {
     __amdgpu_buffer_rsrc_t rs;
     uint32_t sh;                                 // in & 3
     uint32_t z;                                  // compressed length
+    const uint8_t* base;                         // in & ~3
 };
 
 __device__ __forceinline__ Src make_src(const uint8_t* in, uint32_t z)
@@ -103,7 +104,8 @@ __device__ __forceinline__ Src make_src(const uint8_t* in, uint32_t z)
     const uintptr_t base = (((uintptr_t)hi << 32) | lo) & ~(uintptr_t)3;
     const uint32_t sh = lo & 3u;
     const uint32_t bytes = ((sh + z - 1) & ~3u) + 4u;
-    return {__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000), sh, z};
+    return {__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000), sh, z,
+            (const uint8_t*)base};
 }
 
 // 4 input bytes from position pos (any alignment); bytes past z are whatever
@@ -306,6 +308,217 @@ __device__ __forceinline__ uint32_t out_byte(const Out& O, uint32_t pos)
     return (w >> (8 * (pos & 3u))) & 0xFFu;
 }
 
+// ---- the row executor (ROWS): output rows of 256 bytes, 4 per lane ---------
+// Every byte of a row gets an ORIGIN: an LDS byte (ring or staged input,
+// kLdsF), an input position (kInF), or an output position; an output position
+// inside the row is followed by pointer doubling until none is left, then one
+// gather and one ds_write_b32 per lane move the row.
+constexpr uint32_t kLdsF = 0x80000000u;          // origin: LDS byte address
+constexpr uint32_t kInF = 0x40000000u;           // origin: compressed-input position
+constexpr uint32_t kLowM = 0x3FFFFFFFu;
+constexpr uint32_t kRowMax = 1u << 28;           // output positions the origins can carry
+constexpr uint32_t kRowB = 4 * kWave;            // bytes per row
+constexpr uint32_t kTabB = 4 * kRowB;            // the row's origin table (u32 a byte)
+
+__device__ __forceinline__ uint32_t bperm(uint32_t lane4, uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)lane4, (int)v);
+}
+
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// Inclusive running maximum over the wave.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v)
+{
+    v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));
+    v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));
+    v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));
+    v = umax(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));
+    const uint32_t r0 = lane_read(v, 15), r1 = lane_read(v, 31), r2 = lane_read(v, 47);
+    const uint32_t row = lane_id() >> 4;
+    v = row >= 1 ? umax(v, r0) : v;
+    v = row >= 2 ? umax(v, r1) : v;
+    v = row >= 3 ? umax(v, r2) : v;
+    return v;
+}
+
+// The window's output [op, op + span) in rows.  Lane k holds instruction k:
+// its match [ok_, ok_ + L) from d back, then lit literal bytes from lsrc.
+// (diagnostics, STAMPS) cycles: 3 row set-up (flush, starts, scan,
+// descriptors), 5 doubling, 6 LDS gather and row write, 7 HBM / input
+// loads; counts: 10 rows, 11 doubling rounds, 12 rows with HBM or input
+// bytes, 15 rows with 3+ instructions in a lane's 4 bytes
+template <bool STAMPS>
+__device__ __forceinline__ void row_exec(uint8_t* lds, Out& O, const Src& S, uint32_t P, uint32_t so,
+                                         bool act, uint32_t ok_, uint32_t L, uint32_t d, uint32_t lit,
+                                         uint32_t lsrc, uint32_t op, uint32_t span, uint64_t (&acc)[16],
+                                         uint64_t& tmark)
+{
+#define RSTAMP(ph)                                                  \
+    do {                                                            \
+        if (STAMPS) {                                               \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+            acc[ph] += now_ - tmark;                                \
+            tmark = now_;                                           \
+        }                                                           \
+    } while (0)
+#define RCOUNT(i, v)                                                \
+    do {                                                            \
+        if (STAMPS)                                                 \
+            acc[i] += (v);                                          \
+    } while (0)
+    const uint32_t l = lane_id();
+    const uint32_t end = op + span;
+    const uint32_t lS = ok_ + L;                 // the literal part's output start
+    const bool lst = lit != 0 && lsrc >= P && lsrc + lit <= P + kStage;
+    // literal origin = ((litb + p) & kLowM) | (litb & ~kLowM)
+    const uint32_t litb = lst ? ((so + (lsrc - P) - lS) & kLowM) | kLdsF : ((lsrc - lS) & kLowM) | kInF;
+    const bool mk1 = act && L != 0, mk2 = act && lit != 0;
+    uint8_t* const mark = lds + kFarOff;         // segment starts of the row (u8 [256])
+    uint32_t carry = 0;                          // segment covering the row's first byte
+    for (uint32_t R0 = op & ~15u; R0 < end; R0 += kRowB) {
+        // Ring slots: the row [R0, R0 + kRowB), then kTabB bytes of dead slots
+        // (output already in HBM) that hold the row's origin table; output
+        // from R0 + kRowB + kTabB - kRing up is in the ring, older in HBM.
+        if (R0 + kRowB + kTabB - O.stored > kRing)
+            flush_to(lds, O, R0 & ~(kChunk - 1));
+        const uint32_t lim = R0 + kRowB + kTabB - kRing;   // (mod 2^32: compare o + kRing)
+        // segment ids (2k + 1 match of k, 2k + 2 its literals; 0 = a byte this
+        // window does not write) by a running maximum over the row's starts
+        const bool s1 = mk1 && ok_ - R0 < kRowB, s2 = mk2 && lS - R0 < kRowB;
+        uint32_t g[4] = {carry, carry, carry, carry};
+        if (__ballot(s1 || s2)) {
+            // (a row inside one long segment has no start: every byte is carry)
+            *(uint32_t*)(mark + 4 * l) = 0;
+            if (s1)
+                mark[ok_ - R0] = (uint8_t)(2 * l + 1);
+            if (s2)
+                mark[lS - R0] = (uint8_t)(2 * l + 2);
+            const uint32_t mv = *(const uint32_t*)(mark + 4 * l);
+            const uint32_t h0 = mv & 0xFFu;
+            const uint32_t h1 = umax(h0, (mv >> 8) & 0xFFu);
+            const uint32_t h2 = umax(h1, (mv >> 16) & 0xFFu);
+            const uint32_t h3 = umax(h2, mv >> 24);
+            const uint32_t inc = wave_incl_max(h3);
+            const uint32_t pre = umax(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xF, 0xF, true));
+            carry = umax(carry, lane_read(inc, 63));
+            g[0] = umax(pre, h0);
+            g[1] = umax(pre, h1);
+            g[2] = umax(pre, h2);
+            g[3] = umax(pre, h3);
+        }
+        const uint32_t pb = R0 + 4 * l;
+        uint32_t k[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            g[j] = pb + j < end ? g[j] : 0u;
+            k[j] = g[j] ? (g[j] - 1) >> 1 : 0u;
+        }
+        // descriptors of the bytes' instructions: those of bytes 0 and 3 always,
+        // of bytes 1 and 2 when a third instruction starts inside the lane's 4
+        uint32_t D[4], B[4];
+        D[0] = bperm(4 * k[0], d);
+        B[0] = bperm(4 * k[0], litb);
+        D[3] = bperm(4 * k[3], d);
+        B[3] = bperm(4 * k[3], litb);
+        D[1] = k[1] == k[0] ? D[0] : D[3];
+        B[1] = k[1] == k[0] ? B[0] : B[3];
+        D[2] = k[2] == k[3] ? D[3] : D[0];
+        B[2] = k[2] == k[3] ? B[3] : B[0];
+        const bool n1 = k[1] != k[0] && k[1] != k[3], n2 = k[2] != k[0] && k[2] != k[3];
+        RCOUNT(10, 1);
+        if (__ballot(n1 || n2)) {
+            RCOUNT(15, 1);
+            const uint32_t x1 = bperm(4 * k[1], d), y1 = bperm(4 * k[1], litb);
+            const uint32_t x2 = bperm(4 * k[2], d), y2 = bperm(4 * k[2], litb);
+            D[1] = n1 ? x1 : D[1];
+            B[1] = n1 ? y1 : B[1];
+            D[2] = n2 ? x2 : D[2];
+            B[2] = n2 ? y2 : B[2];
+        }
+        // a match byte copies the byte d back (a period shorter than the match
+        // resolves through the doubling below: reducing it to its last
+        // repetition by a modulo measured slower, 0.87 against 0.84 ms on C2)
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t p = pb + j;
+            const uint32_t om = p - D[j], ol = ((B[j] + p) & kLowM) | (B[j] & ~kLowM);
+            // (bitwise selects: a conditional here becomes an exec-masked branch)
+            const uint32_t mz = 0u - (uint32_t)(g[j] != 0), mo = 0u - (g[j] & 1u);
+            o[j] = ((kLdsF | (p & kRingMask)) & ~mz) | (((om & mo) | (ol & ~mo)) & mz);
+        }
+        RSTAMP(3);
+        // pointer doubling over the row's own bytes, through the origin table
+        const uint32_t tb = (R0 + kRowB) & kRingMask;
+        for (;;) {
+            bool q[4];
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                q[j] = (o[j] & (kLdsF | kInF)) == 0 && o[j] >= R0;
+                any = any || q[j];
+            }
+            if (!__ballot(any))
+                break;
+            RCOUNT(11, 1);
+            *(uint4*)(lds + ((tb + 16 * l) & kRingMask)) = make_uint4(o[0], o[1], o[2], o[3]);
+            uint32_t nx[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t t = q[j] ? o[j] - R0 : 4 * l + j;
+                nx[j] = *(const uint32_t*)(lds + ((tb + 4 * t) & kRingMask));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                o[j] = q[j] ? nx[j] : o[j];
+        }
+        RSTAMP(5);
+        // gather: LDS (ring or stage), else HBM (output older than the ring
+        // keeps, read through L2 once this wave's stores landed) or the
+        // compressed input
+        uint32_t v[4];
+        bool gl = false;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const bool lo = (o[j] & kLdsF) != 0;
+            const bool hbm = !lo && !(o[j] & kInF) && o[j] + kRing < lim + kRing;
+            v[j] = lds[lo ? (o[j] & kLowM) : (o[j] & kRingMask)];
+            gl = gl || (o[j] & kInF) || hbm;
+        }
+        RSTAMP(6);
+        if (__ballot(gl)) {
+            RCOUNT(12, 1);
+            // every lane loads 4 dwords (the output's first dword where it has
+            // nothing to fetch), then waits once
+            __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0): this wave's stores landed
+            uint32_t w[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool in = (o[j] & kInF) != 0;
+                const bool hb = !(o[j] & (kLdsF | kInF)) && o[j] + kRing < lim + kRing;
+                const uint32_t a = in ? (o[j] & kLowM) + S.sh : (hb ? o[j] : 0u);
+                const uint8_t* base = in ? S.base : O.out;
+                w[j] = __hip_atomic_load((const uint32_t*)(base + (a & ~3u)), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool in = (o[j] & kInF) != 0;
+                const bool hb = !(o[j] & (kLdsF | kInF)) && o[j] + kRing < lim + kRing;
+                const uint32_t a = in ? (o[j] & kLowM) + S.sh : o[j];
+                const uint32_t x = (w[j] >> (8 * (a & 3u))) & 0xFFu;
+                v[j] = (in || hb) ? x : v[j];
+            }
+            RSTAMP(7);
+        }
+        *(uint32_t*)(lds + (pb & kRingMask)) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        RSTAMP(6);
+    }
+#undef RSTAMP
+#undef RCOUNT
+}
+
 // General execution of one instruction: a match of L bytes from d back at
 // output position x, then lit literal bytes from input position lsrc, in
 // passes of up to 64 bytes with the ring flushed as it fills.
@@ -402,7 +615,7 @@ __device__ __forceinline__ void close_block(uint32_t b, bool ok, uint32_t len, u
 // near matches, 5 far matches, 6 literal-only slow passes, 7 far loads and
 // flushes, 13 executor's barrier waits; counts: 8 windows, 9 instructions,
 // 10 slow near, 11 far, 12 slow literals
-template <bool STAMPS>
+template <bool STAMPS, bool ROWS>
 __global__ __launch_bounds__(2 * kWave, 8) void lzo1x_decode_ser_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
@@ -575,10 +788,13 @@ __global__ __launch_bounds__(2 * kWave, 8) void lzo1x_decode_ser_kernel(
             const uint32_t ok_ = incl - tot + op;            // this instruction's output position
             // capacity (NEED_OP) and look-behind (TEST_LB), lane-parallel
             const bool bad = act && (op + incl > cap || (L != 0 && d > ok_));
-            if (__ballot(bad) != 0 || op + span > cap)
+            if (__ballot(bad) != 0 || op + span > cap || (ROWS && op + span >= kRowMax))
                 ok = false;
             STAMP(2);
-            if (ok) {
+            if (ok && ROWS) {
+                row_exec<STAMPS>(lds, O, S, P, so, act, ok_, L, d, lit, lsrc, op, span, acc, tmark);
+                op += span;
+            } else if (ok) {
                 const bool small = span <= kFastSpan && tot <= kWave &&
                                    (lit == 0 || (lsrc >= P && lsrc + lit <= P + kStage));
                 if (span <= kFastSpan)
@@ -703,7 +919,7 @@ __global__ __launch_bounds__(2 * kWave, 8) void lzo1x_decode_ser_kernel(
     if (STAMPS && l == 0) {
         if (wave == 0) {
             for (int x = 2; x < 16; x++)
-                dbg[(size_t)b * 16 + x] = acc[x];
+                dbg[(size_t)b * 16 + x] = acc[x];   // (14, 15: row executor counts)
         } else {
             dbg[(size_t)b * 16 + 0] = acc[0];
             dbg[(size_t)b * 16 + 1] = acc[1];
@@ -724,7 +940,7 @@ extern "C" int lzo_mi355x_launch_decompress_ser(const uint8_t* src, const uint64
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_decode_ser_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0, stream, src,
+    hipLaunchKernelGGL((lzo1x_decode_ser_kernel<false, false>), dim3(nblocks), dim3(2 * kWave), 0, stream, src,
                        src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback, fallback_ids,
                        nblocks, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -741,8 +957,40 @@ extern "C" int lzo_mi355x_debug_decompress_ser_stamps(const uint8_t* src, const 
 {
     if (nblocks == 0)
         return 0;
-    hipLaunchKernelGGL(lzo1x_decode_ser_kernel<true>, dim3(nblocks), dim3(2 * kWave), 0, stream, src,
+    hipLaunchKernelGGL((lzo1x_decode_ser_kernel<true, false>), dim3(nblocks), dim3(2 * kWave), 0, stream, src,
                        src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback, fallback_ids,
                        nblocks, stamps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The same walker with the row executor (POM_DECODER=row).
+extern "C" int lzo_mi355x_launch_decompress_row(const uint8_t* src, const uint64_t* src_off,
+                                                const uint32_t* src_len, uint8_t* dst,
+                                                const uint64_t* dst_off, const uint32_t* dst_cap,
+                                                uint32_t* out_len, int32_t* status,
+                                                uint32_t* fallback, uint32_t* fallback_ids,
+                                                uint32_t nblocks, hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL((lzo1x_decode_ser_kernel<false, true>), dim3(nblocks), dim3(2 * kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
+                       fallback_ids, nblocks, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzo_mi355x_debug_decompress_row_stamps(const uint8_t* src, const uint64_t* src_off,
+                                                      const uint32_t* src_len, uint8_t* dst,
+                                                      const uint64_t* dst_off, const uint32_t* dst_cap,
+                                                      uint32_t* out_len, int32_t* status,
+                                                      uint32_t* fallback, uint32_t* fallback_ids,
+                                                      uint32_t nblocks, uint64_t* stamps,
+                                                      hipStream_t stream)
+{
+    if (nblocks == 0)
+        return 0;
+    hipLaunchKernelGGL((lzo1x_decode_ser_kernel<true, true>), dim3(nblocks), dim3(2 * kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, fallback,
+                       fallback_ids, nblocks, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -248,14 +248,15 @@ size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
 /* Which throughput decoder a batch uses: the op-set decoder
  * (lzo1x_decode_fast.hip: 16 blocks per CU) or the windowed one
  * (lzo1x_decode_win.hip: 2 blocks per CU, a 64 KiB LDS output ring, never
- * reads its own output back).  POM_DECODER=fast|win forces one; single calls
+ * reads its own output back).  POM_DECODER=fast|win|ser|row forces one (ser,
+ * row: lzo1x_decode_ser.hip); single calls
  * always use the windowed one (see single_call). */
 static int use_win_decoder(uint32_t nblocks)
 {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("POM_DECODER");
-        v = !e ? 3 : strcmp(e, "win") == 0 ? 1 : strcmp(e, "ser") == 0 ? 2 : 0;
+        v = !e ? 3 : strcmp(e, "win") == 0 ? 1 : strcmp(e, "ser") == 0 ? 2 : strcmp(e, "row") == 0 ? 4 : 0;
     }
     if (v != 3)
         return v;
@@ -314,13 +315,14 @@ static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, cons
     const uint32_t nsets = (uint32_t)scr_sets(nblocks);
     uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nblocks));
     if (win) {
-        /* the windowed (win == 1) or table-walk (win == 2) decoder: no op
-         * sets, only the fallback list */
+        /* the windowed (win == 1), table-walk (win == 2) or row (win == 4)
+         * decoder: no op sets, only the fallback list */
         if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
             return -1;
-        if ((win == 2 ? lzo_mi355x_launch_decompress_ser
-                      : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
-                                                          out_len, status, fb, ids, nblocks, s) != 0)
+        if ((win == 2   ? lzo_mi355x_launch_decompress_ser
+             : win == 4 ? lzo_mi355x_launch_decompress_row
+                        : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
+                                                            out_len, status, fb, ids, nblocks, s) != 0)
             return -1;
     } else {
         if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)

@@ -89,6 +89,14 @@ int lzo_mi355x_launch_decompress_ser(const uint8_t *src, const uint64_t *src_off
                                      uint32_t *out_len, int32_t *status, uint32_t *fallback,
                                      uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
 
+/* The table-walk walker with the row executor (lzo1x_decode_ser.hip, ROWS):
+ * output rows of 256 bytes resolved to final origins.  Same arguments. */
+int lzo_mi355x_launch_decompress_row(const uint8_t *src, const uint64_t *src_off,
+                                     const uint32_t *src_len, uint8_t *dst,
+                                     const uint64_t *dst_off, const uint32_t *dst_cap,
+                                     uint32_t *out_len, int32_t *status, uint32_t *fallback,
+                                     uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
+
 /* Unchecked-decoder pre-scan: decoded length and status per block; with
  * cap_out, also min(length, cap_limit) per block (a decode's capacity). */
 int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off,

@@ -1,4 +1,4 @@
-"""A/B of the throughput decoders (fast, win, ser) on one GPU: the round-2 op-set decoder
+"""A/B of the throughput decoders (fast, win, ser, row) on one GPU: the round-2 op-set decoder
 (lzo_mi355x_launch_decompress_fast) and the windowed decoder
 (lzo_mi355x_launch_decompress_win), kernel time by HIP events, output checked.
 Workloads: C2 (4096 x 64 KiB ITB), lone blocks (one 64 KiB, one 536,192 B ITB
@@ -28,6 +28,9 @@ win.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
 ser = lib.lzo_mi355x_launch_decompress_ser
 ser.restype = ctypes.c_int
 ser.argtypes = win.argtypes
+row = lib.lzo_mi355x_launch_decompress_row
+row.restype = ctypes.c_int
+row.argtypes = win.argtypes
 lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
 lib.lzo_mi355x_fast_resident_blocks.restype = ctypes.c_uint32
 p = lambda x: x.data_ptr()
@@ -90,7 +93,7 @@ def run(kind, src, za, zb, zl, nb, reps):
             rc = fast(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
                       p(head), p(ids), p(head) + 256, p(ring), p(ops), nsets, nb, s.cuda_stream)
         else:
-            rc = (ser if kind == "ser" else win)(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
+            rc = {"ser": ser, "row": row}.get(kind, win)(p(za), p(zb.off), p(zl), p(out), p(src.off), p(src.length), p(ol), p(st),
                      p(head), p(ids), nb, s.cuda_stream)
         ev1.record(s)
         torch.cuda.synchronize()

@@ -1,6 +1,7 @@
 """Per-phase cycle stamps of the table-walk decoder (lzo1x_decode_ser.hip,
 lzo_mi355x_debug_decompress_ser_stamps): mean cycles per block of each phase
-for a lone 64 KiB ITB block and for C2 (4096 x 64 KiB), output checked."""
+for a lone 64 KiB ITB block and for C2 (4096 x 64 KiB), output checked.
+--row: the row executor (lzo_mi355x_debug_decompress_row_stamps)."""
 import ctypes
 import os
 import sys
@@ -17,11 +18,14 @@ dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
 lib = lzo.load()
-fn = lib.lzo_mi355x_debug_decompress_ser_stamps
+ROW = "--row" in sys.argv
+fn = lib.lzo_mi355x_debug_decompress_row_stamps if ROW else lib.lzo_mi355x_debug_decompress_ser_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 p = lambda x: x.data_ptr()
 NAMES = ["stage+table", "walk", "decode+scan", "one-pass", "slow near", "far", "slow lits", "flush"]
+if ROW:
+    NAMES = ["stage+table", "walk", "decode+scan", "row set-up", "periodic", "doubling", "gather", "HBM/input"]
 
 
 def run(sizes):
@@ -58,7 +62,11 @@ def run(sizes):
     print(f"blocks {nb}: kernel {ev0.elapsed_time(ev1):.3f} ms, exact {ok}, cycles/block {tot:.0f}")
     for i, nm in enumerate(NAMES):
         print(f"  {nm:12s} {a[i]:10.0f}  {100 * a[i] / tot:5.1f}%")
-    print("  windows %.1f  instructions %.1f  slow near %.1f  far %.1f  slow lits %.1f" % tuple(a[8:13]))
+    if ROW:
+        print("  windows %.1f  instructions %.1f  rows %.1f  doubling rounds %.1f  HBM/input rows %.1f"
+              "  periodic rows %.1f  3+-instruction rows %.1f" % (a[8], a[9], a[10], a[11], a[12], a[14], a[15]))
+    else:
+        print("  windows %.1f  instructions %.1f  slow near %.1f  far %.1f  slow lits %.1f" % tuple(a[8:13]))
     print("  executor barrier waits %.0f cycles/block (walker: stage+table+walk %.0f; executor phases 2-7 %.0f)"
           % (a[13], a[0] + a[1], a[2:8].sum()))
 
