@@ -68,6 +68,8 @@ struct slot {
     size_t dcap;
     uint8_t *hmem;
     size_t hcap;
+    void *lat;                  /* single calls: the latency decoder's scratch */
+    size_t latcap;
 };
 
 /* A host thread's resources on one device: kSlots slots, so that several
@@ -104,6 +106,8 @@ static void tctx_free(void *p)
                 hipFree(c->s[k].dmem);
             if (c->s[k].hmem)
                 hipHostFree(c->s[k].hmem);
+            if (c->s[k].lat)
+                hipFree(c->s[k].lat);
             hipStreamDestroy(c->s[k].stream);
         }
     }
@@ -1016,6 +1020,41 @@ static struct slot *sc_slot(struct sc_queue *q)
     return &q->slot;
 }
 
+/* A lone decode whose compressed block is at least this long takes the
+ * latency decoder (lzo1x_decode_lat.hip: the whole GPU on one block, ~0.22 ms
+ * from 64 KiB up to 536 KB, where the windowed decoder's one workgroup takes
+ * 0.27-2.2 ms); shorter ones the windowed decoder.  POM_SC_LAT_MIN sets the
+ * threshold (bytes of compressed input), POM_SC_LAT=0 turns it off. */
+static int use_lat_decoder(size_t z)
+{
+    static long min_z = -1;
+    if (min_z < 0) {
+        const char *off = getenv("POM_SC_LAT");
+        const char *e = getenv("POM_SC_LAT_MIN");
+        min_z = off && strcmp(off, "0") == 0 ? 0x7FFFFFFFL : e && atol(e) > 0 ? atol(e) : 7000L;
+    }
+    return z >= (size_t)min_z;
+}
+
+static int lat_reserve(struct slot *t, size_t bytes)
+{
+    if (t->latcap >= bytes)
+        return 0;
+    if (t->lat) {
+        hipStreamSynchronize(t->stream);
+        hipFree(t->lat);
+        t->lat = NULL;
+        t->latcap = 0;
+    }
+    const size_t want = ALIGN_UP(bytes + bytes / 4, (size_t)1 << 20);
+    if (hipMalloc(&t->lat, want) != hipSuccess) {
+        t->lat = NULL;
+        return -1;
+    }
+    t->latcap = want;
+    return 0;
+}
+
 static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
 {
     const enum sc_kind kind = g[0]->kind;
@@ -1073,8 +1112,16 @@ static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
          * OUTPUT_OVERRUN here means the stream is longer than the room.
          * The windowed decoder never reads its output back (host memory);
          * its fallback list lives in the header (zeroed by the H2D copy). */
-        rc = lzo_mi355x_launch_decompress_win(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap,
-                                              olen, ost, dh.fb, dh.fb + 1, (uint32_t)k, s);
+        int lat = 0;
+        if (k == 1 && use_lat_decoder(g[0]->src_len) && g[0]->room <= 0xFFFFFFFFu) {
+            const uint32_t z = (uint32_t)g[0]->src_len, cap = (uint32_t)g[0]->room;
+            lat = lat_reserve(t, lzo_mi355x_decompress_lat_scratch(z, cap)) == 0 &&
+                  lzo_mi355x_launch_decompress_lat(d + o_src[0], z, out + o_out[0], cap, olen, ost, dh.fb,
+                                                   dh.fb + 1, 0, t->lat, t->latcap, s) == 0;
+        }
+        rc = lat ? 0
+                 : lzo_mi355x_launch_decompress_win(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap,
+                                                    olen, ost, dh.fb, dh.fb + 1, (uint32_t)k, s);
     }
     /* (copy mode: lengths and statuses, then the outputs) */
     if (rc != 0 ||

@@ -115,3 +115,42 @@ def gpu_decompress_win(torch, comps: Sequence[bytes], caps: Sequence[int], dev, 
     torch.cuda.synchronize()
     nfb = int(head[0].item())
     return fetch(dst, olen, cap=caps), st.cpu().numpy().tolist(), sorted(ids[:nfb].cpu().numpy().tolist())
+
+
+def gpu_decompress_lat(torch, comps: Sequence[bytes], caps: Sequence[int], dev):
+    """The latency decoder (lzo_mi355x_launch_decompress_lat) alone, one block
+    per pipeline, without the exact decoder behind it.  Returns the outputs,
+    statuses and the ids of the blocks it handed over; a block outside its
+    range (the launcher returns -1) is reported with status None."""
+    import ctypes
+    lib = lzo.load()
+    fn = lib.lzo_mi355x_launch_decompress_lat
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    sz = lib.lzo_mi355x_decompress_lat_scratch
+    sz.restype = ctypes.c_size_t
+    sz.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    src = device_batch(torch, comps, dev)
+    dst = empty_batch(torch, caps, dev, fill=0x5A)
+    n = len(comps)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    head = torch.zeros(64, dtype=torch.int32, device=dev)
+    ids = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+    p = lambda x: x.data_ptr()
+    s = torch.cuda.current_stream().cuda_stream
+    soff = src.off.cpu().numpy()
+    doff = dst.off.cpu().numpy()
+    launched = []
+    for i, (z, cap) in enumerate(zip(comps, caps)):
+        need = int(sz(len(z), int(cap))) if len(z) else 0
+        scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        rc = fn(p(src.arena) + int(soff[i]), len(z), p(dst.arena) + int(doff[i]), int(cap),
+                p(olen), p(st), p(head), p(ids), i, p(scratch), need, s)
+        torch.cuda.synchronize()
+        launched.append(rc == 0)
+    nfb = int(head[0].item())
+    sts = [x if ok else None for x, ok in zip(st.cpu().numpy().tolist(), launched)]
+    return fetch(dst, olen, cap=caps), sts, sorted(ids[:nfb].cpu().numpy().tolist())
