@@ -22,9 +22,9 @@
 //  4. ORIGINS: output byte p is covered by the instruction whose start is the
 //     running maximum of starts at p; its origin is an input position (a
 //     literal) or p - d (a match byte).
-//  5. DOUBLING: origin[p] = origin[origin[p]] until every origin is a literal
-//     (chains on ITB blocks are at most ~600 hops: <= 10 rounds; a round that
-//     finds nothing left ends the rest early).
+//  5. DOUBLING: origin[p] = origin applied 8 times, until every origin is a
+//     literal (chains on ITB blocks are at most ~600 hops: <= 4 rounds; a
+//     round that finds nothing left ends the rest early).
 //  6. GATHER: out[p] = in[origin[p]].
 // Every stage is a plain grid over nodes or output bytes; the scans are
 // two-level (tiles of 4096, then the tile totals).
@@ -146,6 +146,8 @@ __device__ Ins decode_at(const uint8_t* in, uint32_t z, uint32_t p, uint32_t s)
     return x;
 }
 
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
 // node ids: 0 = position 0 in state F; 1 + 2i + c = position i, class c (0 A,
 // 1 B/C); END = 2z + 1; BAD = 2z + 2
 __device__ __forceinline__ void node_pos(uint32_t id, uint32_t& p, uint32_t& s)
@@ -155,9 +157,14 @@ __device__ __forceinline__ void node_pos(uint32_t id, uint32_t& p, uint32_t& s)
 }
 
 __global__ __launch_bounds__(kT) void lat_nodes(const uint8_t* __restrict__ in, uint32_t z, uint32_t* __restrict__ J0,
-                                                uint32_t* __restrict__ nst, uint32_t* __restrict__ mark)
+                                                uint32_t* __restrict__ nst, uint32_t* __restrict__ mark,
+                                                uint32_t* __restrict__ ctl, uint32_t* __restrict__ cover, uint32_t cap)
 {
     const uint32_t N = 2 * z + 3, END = 2 * z + 1, BAD = 2 * z + 2;
+    if (blockIdx.x == 0 && threadIdx.x < C_ROUND + kRounds)
+        ctl[threadIdx.x] = 0;
+    for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < cap; p += gridDim.x * kT)
+        cover[p] = 0;
     for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT) {
         uint32_t j = id, ns = ST_A;
         if (id < END) {
@@ -173,19 +180,52 @@ __global__ __launch_bounds__(kT) void lat_nodes(const uint8_t* __restrict__ in, 
     }
 }
 
-__global__ __launch_bounds__(kT) void lat_jump(const uint32_t* __restrict__ Jp, uint32_t* __restrict__ Jn, uint32_t N)
+// levels k + 1 .. k + nl (nl <= 3) from level k: J_{k+i} = J_k applied 2^i
+// times (one launch per three levels: launches, not work, bound this path)
+__global__ __launch_bounds__(kT) void lat_jump(const uint32_t* __restrict__ Jk, uint32_t* __restrict__ Jn, uint32_t N,
+                                               uint32_t nl)
 {
-    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT)
-        Jn[id] = Jp[Jp[id]];
+    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT) {
+        uint32_t x = Jk[Jk[id]];
+        Jn[id] = x;
+        if (nl > 1) {
+            x = Jk[Jk[x]];
+            Jn[(size_t)N + id] = x;
+        }
+        if (nl > 2) {
+            x = Jk[Jk[Jk[Jk[x]]]];
+            Jn[2 * (size_t)N + id] = x;
+        }
+    }
 }
 
-// nodes reached from a marked node by 2^k steps are marked (marks made in the
+// levels k, k - 1, k - 2 (nl of them, from the top): every node reached from a
+// marked node by any combination of those jumps is marked (marks made in the
 // same pass may propagate further: still nodes of the path)
-__global__ __launch_bounds__(kT) void lat_mark(const uint32_t* __restrict__ Jk, uint32_t* mark, uint32_t N)
+__global__ __launch_bounds__(kT) void lat_mark(const uint32_t* __restrict__ J, uint32_t* mark, uint32_t N, uint32_t k,
+                                               uint32_t nl)
 {
-    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT)
-        if (__hip_atomic_load(mark + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            __hip_atomic_store(mark + Jk[id], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* J0 = J + (size_t)k * N;
+    const uint32_t* J1 = J0 - (nl > 1 ? N : 0);
+    const uint32_t* J2 = J1 - (nl > 2 ? N : 0);
+    auto set = [&](uint32_t x) { __hip_atomic_store(mark + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT) {
+        if (!__hip_atomic_load(mark + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            continue;
+        const uint32_t a = J0[id];
+        set(a);
+        if (nl > 1) {
+            const uint32_t b = J1[id], c = J1[a];
+            set(b);
+            set(c);
+            if (nl > 2) {
+                set(J2[id]);
+                set(J2[a]);
+                set(J2[b]);
+                set(J2[c]);
+            }
+        }
+    }
 }
 
 // running-maximum input: the id of every instruction node, 0 elsewhere
@@ -250,7 +290,8 @@ __global__ __launch_bounds__(kT) void lat_starts(const uint32_t* __restrict__ ma
     }
 }
 
-__global__ __launch_bounds__(kT) void lat_origins(const uint32_t* __restrict__ cover, const uint4* __restrict__ fld,
+__global__ __launch_bounds__(kT) void lat_origins(const uint32_t* __restrict__ cover, const uint32_t* __restrict__ tiles,
+                                                  const uint4* __restrict__ fld,
                                                   const uint32_t* __restrict__ tot, const uint32_t* __restrict__ osum,
                                                   uint32_t* __restrict__ org, const uint32_t* __restrict__ ctl)
 {
@@ -258,7 +299,9 @@ __global__ __launch_bounds__(kT) void lat_origins(const uint32_t* __restrict__ c
         return;
     const uint32_t total = ctl[C_TOTAL];
     for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < total; p += gridDim.x * kT) {
-        const uint32_t id = cover[p];
+        uint32_t id = cover[p];
+        if (p >= kTile)
+            id = umax32(tiles[p / kTile], id);   // (the cover scan's add pass)
         const uint4 f = fld[id];
         const uint32_t o = osum[id] - tot[id];
         const uint32_t r = p - o;
@@ -275,11 +318,15 @@ __global__ __launch_bounds__(kT) void lat_double(uint32_t* org, uint32_t* __rest
     const uint32_t total = ctl[C_TOTAL];
     bool left = false;
     for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < total; p += gridDim.x * kT) {
-        const uint32_t o = __hip_atomic_load(org + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t o = __hip_atomic_load(org + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!(o & kLitO)) {
-            const uint32_t o2 = __hip_atomic_load(org + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(org + p, o2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            left = left || !(o2 & kLitO);
+            // seven dereferences a pass: a chain shrinks 8x per launch
+#pragma unroll
+            for (int i = 0; i < 7; i++)
+                if (!(o & kLitO))
+                    o = __hip_atomic_load(org + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(org + p, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            left = left || !(o & kLitO);
         }
     }
     if (__any(left) && (threadIdx.x & 63u) == 0)
@@ -290,9 +337,9 @@ __global__ __launch_bounds__(kT) void lat_gather(const uint8_t* __restrict__ in,
                                                  const uint32_t* __restrict__ org, uint32_t* __restrict__ ctl,
                                                  uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
                                                  uint32_t* __restrict__ fallback, uint32_t* __restrict__ fallback_ids,
-                                                 uint32_t b)
+                                                 uint32_t b, uint32_t rounds)
 {
-    const bool bad = ctl[C_BAD] || ctl[C_ROUND + kRounds - 1];
+    const bool bad = ctl[C_BAD] || ctl[C_ROUND + rounds - 1];
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (bad) {
             out_len[b] = 0xFA110000u;
@@ -390,8 +437,12 @@ __global__ __launch_bounds__(kT) void scan_add(uint32_t* out, uint32_t n, const 
             out[i] = op2<MAX>(tiles[i / kTile], out[i]);
 }
 
+// add = false: the tiles are scanned and their exclusive prefixes left in
+// tiles[] for the consumer to apply (element i: op(tiles[i / kTile], out[i])
+// from the second tile on)
 template <bool MAX>
-int scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tiles, uint32_t grid, hipStream_t s)
+int scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tiles, uint32_t grid, hipStream_t s,
+         bool add = true)
 {
     const uint32_t nt = (n + kTile - 1) / kTile;
     if (nt > kMaxTiles)
@@ -399,7 +450,8 @@ int scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tiles, uint32_
     hipLaunchKernelGGL(scan_tiles<MAX>, dim3(nt), dim3(kScanT), 0, s, in, out, n, tiles);
     if (nt > 1) {
         hipLaunchKernelGGL(scan_tile_totals<MAX>, dim3(1), dim3(kScanT), 0, s, tiles, nt);
-        hipLaunchKernelGGL(scan_add<MAX>, dim3(grid), dim3(kT), 0, s, out, n, (const uint32_t*)tiles);
+        if (add)
+            hipLaunchKernelGGL(scan_add<MAX>, dim3(grid), dim3(kT), 0, s, out, n, (const uint32_t*)tiles);
     }
     return 0;
 }
@@ -474,15 +526,17 @@ extern "C" int lzo_mi355x_launch_decompress_lat(const uint8_t* in, uint32_t z, u
     uint32_t* org = (uint32_t*)(S + L.org);
     auto grid = [](uint32_t n) { uint32_t g = (n + kT - 1) / kT; return g < 1 ? 1u : (g > 4096u ? 4096u : g); };
     const uint32_t gN = grid(N), gC = grid(cap);
-    if (hipMemsetAsync(ctl, 0, (C_ROUND + kRounds) * 4, s) != hipSuccess ||
-        hipMemsetAsync(cover, 0, (size_t)cap * 4, s) != hipSuccess)
-        return -1;
-    hipLaunchKernelGGL(lat_nodes, dim3(gN), dim3(kT), 0, s, in, z, J, nst, mark);
-    for (uint32_t k = 1; k < K; k++)
-        hipLaunchKernelGGL(lat_jump, dim3(gN), dim3(kT), 0, s, (const uint32_t*)(J + (size_t)(k - 1) * N),
-                           J + (size_t)k * N, N);
-    for (uint32_t k = K; k-- > 0;)
-        hipLaunchKernelGGL(lat_mark, dim3(gN), dim3(kT), 0, s, (const uint32_t*)(J + (size_t)k * N), mark, N);
+    hipLaunchKernelGGL(lat_nodes, dim3(gN > gC ? gN : gC), dim3(kT), 0, s, in, z, J, nst, mark, ctl, cover, cap);
+    for (uint32_t k = 0; k + 1 < K; k += 3) {
+        const uint32_t nl = K - 1 - k < 3 ? K - 1 - k : 3u;
+        hipLaunchKernelGGL(lat_jump, dim3(gN), dim3(kT), 0, s, (const uint32_t*)(J + (size_t)k * N),
+                           J + (size_t)(k + 1) * N, N, nl);
+    }
+    for (uint32_t top = K; top > 0;) {
+        const uint32_t nl = top < 3 ? top : 3u;
+        hipLaunchKernelGGL(lat_mark, dim3(gN), dim3(kT), 0, s, (const uint32_t*)J, mark, N, top - 1, nl);
+        top -= nl;
+    }
     hipLaunchKernelGGL(lat_pred_in, dim3(gN), dim3(kT), 0, s, (const uint32_t*)mark, v, z, ctl);
     if (scan<true>(v, pmax, N, tiles, gN, s) != 0)
         return -1;
@@ -492,13 +546,18 @@ extern "C" int lzo_mi355x_launch_decompress_lat(const uint8_t* in, uint32_t z, u
         return -1;
     hipLaunchKernelGGL(lat_starts, dim3(gN), dim3(kT), 0, s, (const uint32_t*)mark, (const uint4*)fld,
                        (const uint32_t*)tot, (const uint32_t*)osum, z, cap, cover, ctl);
-    if (scan<true>(cover, cover, cap, tiles, gC, s) != 0)
+    if (scan<true>(cover, cover, cap, tiles, gC, s, false) != 0)
         return -1;
-    hipLaunchKernelGGL(lat_origins, dim3(gC), dim3(kT), 0, s, (const uint32_t*)cover, (const uint4*)fld,
+    hipLaunchKernelGGL(lat_origins, dim3(gC), dim3(kT), 0, s, (const uint32_t*)cover, (const uint32_t*)tiles,
+                       (const uint4*)fld,
                        (const uint32_t*)tot, (const uint32_t*)osum, org, (const uint32_t*)ctl);
-    for (uint32_t r = 0; r < kRounds; r++)
+    // chains are shorter than cap: 8^R > cap rounds at most
+    uint32_t R = 1;
+    while (R < kRounds && (1ull << (3 * R)) <= (uint64_t)cap)
+        R++;
+    for (uint32_t r = 0; r < R; r++)
         hipLaunchKernelGGL(lat_double, dim3(gC), dim3(kT), 0, s, org, ctl, r);
     hipLaunchKernelGGL(lat_gather, dim3(gC), dim3(kT), 0, s, in, out, (const uint32_t*)org, ctl, out_len, status,
-                       fallback, fallback_ids, b);
+                       fallback, fallback_ids, b, R);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1021,9 +1021,9 @@ static struct slot *sc_slot(struct sc_queue *q)
 }
 
 /* A lone decode whose compressed block is at least this long takes the
- * latency decoder (lzo1x_decode_lat.hip: the whole GPU on one block, ~0.22 ms
- * from 64 KiB up to 536 KB, where the windowed decoder's one workgroup takes
- * 0.27-2.2 ms); shorter ones the windowed decoder.  POM_SC_LAT_MIN sets the
+ * latency decoder (lzo1x_decode_lat.hip: the whole GPU on one block, 0.11-0.14
+ * ms from 32 KiB up to 536 KB, where the windowed decoder's one workgroup takes
+ * 0.14-2.2 ms); shorter ones (equal at 12 KB) the windowed decoder.  POM_SC_LAT_MIN sets the
  * threshold (bytes of compressed input), POM_SC_LAT=0 turns it off. */
 static int use_lat_decoder(size_t z)
 {
@@ -1031,7 +1031,7 @@ static int use_lat_decoder(size_t z)
     if (min_z < 0) {
         const char *off = getenv("POM_SC_LAT");
         const char *e = getenv("POM_SC_LAT_MIN");
-        min_z = off && strcmp(off, "0") == 0 ? 0x7FFFFFFFL : e && atol(e) > 0 ? atol(e) : 7000L;
+        min_z = off && strcmp(off, "0") == 0 ? 0x7FFFFFFFL : e && atol(e) > 0 ? atol(e) : 2048L;
     }
     return z >= (size_t)min_z;
 }

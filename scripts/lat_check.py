@@ -44,7 +44,7 @@ def timed(fn, reps=7):
     return float(np.median(ts))
 
 
-for n in (65536, 262144, 536192):
+for n in (12416, 32768, 65536, 262144, 536192):
     data = synth.block(synth.ITB, 4242 + n, n)
     src = t(np.frombuffer(data, dtype=np.uint8))
     cap = lzo.worst_compress(n)
