@@ -1036,6 +1036,10 @@ static int use_lat_decoder(size_t z)
     return z >= (size_t)min_z;
 }
 
+/* the latency decoder's scratch per slot at most (a block needing more, from
+ * ~4 MB of compressed input, takes the windowed decoder) */
+static const size_t kLatMaxScratch = (size_t)1 << 30;
+
 static int lat_reserve(struct slot *t, size_t bytes)
 {
     if (t->latcap >= bytes)
@@ -1115,7 +1119,8 @@ static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
         int lat = 0;
         if (k == 1 && use_lat_decoder(g[0]->src_len) && g[0]->room <= 0xFFFFFFFFu) {
             const uint32_t z = (uint32_t)g[0]->src_len, cap = (uint32_t)g[0]->room;
-            lat = lat_reserve(t, lzo_mi355x_decompress_lat_scratch(z, cap)) == 0 &&
+            const size_t need = lzo_mi355x_decompress_lat_scratch(z, cap);
+            lat = need <= kLatMaxScratch && lat_reserve(t, need) == 0 &&
                   lzo_mi355x_launch_decompress_lat(d + o_src[0], z, out + o_out[0], cap, olen, ost, dh.fb,
                                                    dh.fb + 1, 0, t->lat, t->latcap, s) == 0;
         }
