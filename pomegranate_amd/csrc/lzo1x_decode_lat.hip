@@ -493,9 +493,17 @@ Lay layout(uint32_t z, uint32_t cap)
 
 }  // namespace
 
+static bool in_range(uint32_t z, uint32_t cap)
+{
+    const uint64_t lim = (uint64_t)kMaxTiles * kTile;   // elements one two-level scan takes
+    return z != 0 && cap != 0 && (uint64_t)2 * z + 3 <= lim && (uint64_t)cap <= lim;
+}
+
+// 0: the block is outside the decoder's range (empty input or room, or more
+// than the scans take)
 extern "C" size_t lzo_mi355x_decompress_lat_scratch(uint32_t z, uint32_t cap)
 {
-    return layout(z, cap).end;
+    return in_range(z, cap) ? layout(z, cap).end : 0;
 }
 
 // One block: in (z bytes) -> out (capacity cap); out_len[b] / status[b] as the
@@ -505,7 +513,7 @@ extern "C" int lzo_mi355x_launch_decompress_lat(const uint8_t* in, uint32_t z, u
                                                 uint32_t* fallback_ids, uint32_t b, void* scratch,
                                                 size_t scratch_bytes, hipStream_t s)
 {
-    if (z == 0 || (uint64_t)2 * z + 3 > (uint64_t)kMaxTiles * kTile || (uint64_t)cap > (uint64_t)kMaxTiles * kTile)
+    if (!in_range(z, cap))
         return -1;
     const Lay L = layout(z, cap);
     if (L.end > scratch_bytes)

@@ -1107,8 +1107,8 @@ static int lat_group(struct slot *t, struct sc_req **g, int k, const uint8_t *d,
         if (!use_lat_decoder(g[i]->src_len) || g[i]->room > 0xFFFFFFFFu)
             return 0;
         const size_t n = lzo_mi355x_decompress_lat_scratch((uint32_t)g[i]->src_len, (uint32_t)g[i]->room);
-        if (n > kLatMaxScratch)
-            return 0;
+        if (n == 0 || n > kLatMaxScratch)
+            return 0;                           /* out of its range: the windowed decoder */
         if (n > need[i % nl])
             need[i % nl] = n;
     }

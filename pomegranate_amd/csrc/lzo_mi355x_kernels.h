@@ -100,9 +100,10 @@ int lzo_mi355x_launch_decompress_row(const uint8_t *src, const uint64_t *src_off
 /* Latency decoder (lzo1x_decode_lat.hip): ONE block of z compressed bytes
  * into out (capacity cap) by a pipeline of grid-wide kernels; out_len[b] /
  * status[b] and the fallback list as above.  scratch: at least
- * lzo_mi355x_decompress_lat_scratch(z, cap) bytes of device memory.  Returns -1
- * (nothing launched) when the block is outside its range (2z + 3 or cap over
- * 16 Mi, or too little scratch). */
+ * lzo_mi355x_decompress_lat_scratch(z, cap) bytes of device memory (0: the
+ * block is outside the decoder's range -- z or cap 0, 2z + 3 or cap over
+ * 16 Mi).  Returns -1 (nothing launched) outside that range or with too little
+ * scratch. */
 size_t lzo_mi355x_decompress_lat_scratch(uint32_t z, uint32_t cap);
 int lzo_mi355x_launch_decompress_lat(const uint8_t *in, uint32_t z, uint8_t *out, uint32_t cap,
                                      uint32_t *out_len, int32_t *status, uint32_t *fallback,

@@ -747,3 +747,26 @@ def test_latency_decoder_hands_over_malformed_and_short_room(dev, gu, malformed)
     comps2, _ = gu.gpu_compress(torch, blocks, dev)
     outs2, st2, handed2 = gu.gpu_decompress_lat(torch, comps2, [65535] * 3, dev)
     assert handed2 == [0, 1, 2] and st2 == [0x7FFF0001] * 3
+
+
+def test_lone_single_calls_on_the_latency_decoder(dev, oracle):
+    """Lone lzo1x_decompress / lzo1x_decompress_safe calls of 2 KB or more of
+    compressed input take the latency decoder (lzo_host.c lat_group): exact
+    bytes and lengths from 8 KB to 536,192 B, OUTPUT_OVERRUN for a room one
+    byte short and for no room at all, and a malformed stream's code from the
+    exact decoder behind it, as the reference (lib/minilzo.c:3703-4190)."""
+    for i, n in enumerate((8192, 65536, 200000, 536192)):
+        d = synth.block(synth.ITB if i % 2 else synth.TEXT, 5151 + i, n)
+        z = oracle.compress(d)
+        assert len(z) >= 2048
+        rc, back = lzo.lzo1x_decompress(z)
+        assert rc == 0 and back == d
+        rc, back = lzo.lzo1x_decompress_safe(z, n)
+        assert rc == 0 and back == d
+        rc, _ = lzo.lzo1x_decompress_safe(z, n - 1)
+        assert rc == lzo.LZO_E_OUTPUT_OVERRUN
+        rc, _ = lzo.lzo1x_decompress_safe(z, 0)
+        assert rc == lzo.LZO_E_OUTPUT_OVERRUN
+        cut = z[: len(z) // 2]
+        rc, _ = lzo.lzo1x_decompress_safe(cut, n)
+        assert rc == oracle.decompress_safe(cut, n)[0]
