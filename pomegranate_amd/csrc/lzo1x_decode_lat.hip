@@ -46,7 +46,41 @@ constexpr uint32_t kMaxTiles = kTile;            // one tile of tile totals
 constexpr uint32_t kRounds = 24;                 // doubling rounds at most (chains < 2^24)
 
 // control words in scratch
-enum { C_BAD = 0, C_TOTAL = 1, C_ROUND = 2 };    // C_ROUND + r: round r found work
+constexpr uint32_t kMaxBlk = 8;                  // blocks one pipeline decodes side by side
+// control words in scratch: C_ROUND + r: round r found work; per block b:
+// C_BADB + b handed over, C_TOTB + b output length, C_BASEB + b output sum
+// before its first node
+enum { C_ROUND = 0, C_BADB = 24, C_TOTB = C_BADB + 8, C_BASEB = C_TOTB + 8, C_WORDS = C_BASEB + 8 };
+static_assert(C_BADB >= 24 && kMaxBlk == 8, "control layout");
+
+// The blocks of one pipeline (kernel argument): node ids no .. no + 2z + 2
+// (0 the first byte in state F, 1 + 2i + c position i class c, 2z + 1 END,
+// 2z + 2 BAD), output slots oo .. oo + cap of the flattened output space,
+// input and output at src + in_off, dst + out_off.
+struct BlkMeta {
+    uint32_t no, z, oo, cap;
+    uint64_t in_off, out_off;
+};
+struct Blks {
+    uint32_t nb, N, C, pad;
+    BlkMeta m[kMaxBlk];
+};
+
+__device__ __forceinline__ uint32_t blk_of_node(const Blks& B, uint32_t id)
+{
+    uint32_t b = 0;
+    for (uint32_t i = 1; i < B.nb; i++)
+        b = id >= B.m[i].no ? i : b;
+    return b;
+}
+
+__device__ __forceinline__ uint32_t blk_of_out(const Blks& B, uint32_t p)
+{
+    uint32_t b = 0;
+    for (uint32_t i = 1; i < B.nb; i++)
+        b = p >= B.m[i].oo ? i : b;
+    return b;
+}
 
 struct Ins {
     uint32_t L, d, lit, lsrc, next, nst, kind;   // kind: 0 ok, 1 EOF exactly at z, 2 refuse
@@ -156,27 +190,28 @@ __device__ __forceinline__ void node_pos(uint32_t id, uint32_t& p, uint32_t& s)
     s = id ? (((id - 1) & 1u) ? ST_B : ST_A) : ST_F;
 }
 
-__global__ __launch_bounds__(kT) void lat_nodes(const uint8_t* __restrict__ in, uint32_t z, uint32_t* __restrict__ J0,
+__global__ __launch_bounds__(kT) void lat_nodes(const uint8_t* __restrict__ src, const Blks B, uint32_t* __restrict__ J0,
                                                 uint32_t* __restrict__ nst, uint32_t* __restrict__ mark,
-                                                uint32_t* __restrict__ ctl, uint32_t* __restrict__ cover, uint32_t cap)
+                                                uint32_t* __restrict__ ctl, uint32_t* __restrict__ cover)
 {
-    const uint32_t N = 2 * z + 3, END = 2 * z + 1, BAD = 2 * z + 2;
-    if (blockIdx.x == 0 && threadIdx.x < C_ROUND + kRounds)
-        ctl[threadIdx.x] = 0;
-    for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < cap; p += gridDim.x * kT)
+    const uint32_t g = blockIdx.x * kT + threadIdx.x, step = gridDim.x * kT;
+    if (g < C_WORDS)
+        ctl[g] = 0;
+    for (uint32_t p = g; p < B.C; p += step)
         cover[p] = 0;
-    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT) {
+    for (uint32_t id = g; id < B.N; id += step) {
+        const uint32_t b = blk_of_node(B, id), no = B.m[b].no, z = B.m[b].z, l = id - no;
         uint32_t j = id, ns = ST_A;
-        if (id < END) {
+        if (l < 2 * z + 1) {
             uint32_t p, s;
-            node_pos(id, p, s);
-            const Ins x = decode_at(in, z, p, s);
-            j = x.kind == 2 ? BAD : x.kind == 1 ? END : 1 + 2 * x.next + (x.nst != ST_A ? 1u : 0u);
+            node_pos(l, p, s);
+            const Ins x = decode_at(src + B.m[b].in_off, z, p, s);
+            j = no + (x.kind == 2 ? 2 * z + 2 : x.kind == 1 ? 2 * z + 1 : 1 + 2 * x.next + (x.nst != ST_A ? 1u : 0u));
             ns = x.nst;
         }
         J0[id] = j;
         nst[id] = ns;
-        mark[id] = id == 0 ? 1u : 0u;
+        mark[id] = l == 0 ? 1u : 0u;
     }
 }
 
@@ -228,35 +263,41 @@ __global__ __launch_bounds__(kT) void lat_mark(const uint32_t* __restrict__ J, u
     }
 }
 
-// running-maximum input: the id of every instruction node, 0 elsewhere
-__global__ __launch_bounds__(kT) void lat_pred_in(const uint32_t* __restrict__ mark, uint32_t* __restrict__ v,
-                                                  uint32_t z, uint32_t* __restrict__ ctl)
+// running-maximum input: the id of every instruction node, 0 elsewhere; a
+// block whose path ends anywhere but its END is handed over
+__global__ __launch_bounds__(kT) void lat_pred_in(const Blks B, const uint32_t* __restrict__ mark,
+                                                  uint32_t* __restrict__ v, uint32_t* __restrict__ ctl)
 {
-    const uint32_t N = 2 * z + 3, END = 2 * z + 1, BAD = 2 * z + 2;
-    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT)
-        v[id] = (id < END && mark[id]) ? id : 0u;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (mark[BAD] || !mark[END]))
-        ctl[C_BAD] = 1;
+    const uint32_t g = blockIdx.x * kT + threadIdx.x;
+    for (uint32_t id = g; id < B.N; id += gridDim.x * kT) {
+        const uint32_t b = blk_of_node(B, id);
+        v[id] = (id - B.m[b].no < 2 * B.m[b].z + 1 && mark[id]) ? id : 0u;
+    }
+    if (g < B.nb) {
+        const uint32_t e = B.m[g].no + 2 * B.m[g].z + 1;
+        if (mark[e + 1] || !mark[e])
+            ctl[C_BADB + g] = 1;
+    }
 }
 
 // exact state, fields and output length of every instruction node
-__global__ __launch_bounds__(kT) void lat_fields(const uint8_t* __restrict__ in, uint32_t z,
+__global__ __launch_bounds__(kT) void lat_fields(const uint8_t* __restrict__ src, const Blks B,
                                                  const uint32_t* __restrict__ mark, const uint32_t* __restrict__ pmax,
                                                  const uint32_t* __restrict__ nst, uint4* __restrict__ fld,
                                                  uint32_t* __restrict__ tot, uint32_t* __restrict__ ctl)
 {
-    const uint32_t N = 2 * z + 3, END = 2 * z + 1;
-    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT) {
+    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < B.N; id += gridDim.x * kT) {
+        const uint32_t b = blk_of_node(B, id), z = B.m[b].z, l = id - B.m[b].no;
         uint32_t n = 0;
-        if (id < END && mark[id]) {
+        if (l < 2 * z + 1 && mark[id]) {
             uint32_t p, s;
-            node_pos(id, p, s);
-            if (id != 0)
+            node_pos(l, p, s);
+            if (l != 0)
                 s = nst[pmax[id - 1]];           // the predecessor's next state
-            const Ins x = decode_at(in, z, p, s);
-            const bool cls_a = ((id - 1) & 1u) == 0u;
-            if (x.kind == 2 || (id != 0 && (s == ST_A) != cls_a))
-                ctl[C_BAD] = 1;                  // (a path is consistent by construction)
+            const Ins x = decode_at(src + B.m[b].in_off, z, p, s);
+            const bool cls_a = ((l - 1) & 1u) == 0u;
+            if (x.kind == 2 || (l != 0 && (s == ST_A) != cls_a))
+                ctl[C_BADB + b] = 1;             // (a path is consistent by construction)
             fld[id] = make_uint4(x.L, x.d, x.lit, x.lsrc);
             n = x.L + x.lit;
         }
@@ -264,60 +305,64 @@ __global__ __launch_bounds__(kT) void lat_fields(const uint8_t* __restrict__ in,
     }
 }
 
-// checks (capacity, look-behind) and the start marker of every instruction
-__global__ __launch_bounds__(kT) void lat_starts(const uint32_t* __restrict__ mark, const uint4* __restrict__ fld,
-                                                 const uint32_t* __restrict__ tot, const uint32_t* __restrict__ osum,
-                                                 uint32_t z, uint32_t cap, uint32_t* __restrict__ cover,
+// checks (capacity, look-behind), each block's length, and the start marker
+// of every instruction
+__global__ __launch_bounds__(kT) void lat_starts(const Blks B, const uint32_t* __restrict__ mark,
+                                                 const uint4* __restrict__ fld, const uint32_t* __restrict__ tot,
+                                                 const uint32_t* __restrict__ osum, uint32_t* __restrict__ cover,
                                                  uint32_t* __restrict__ ctl)
 {
-    const uint32_t N = 2 * z + 3, END = 2 * z + 1;
-    const uint32_t total = osum[N - 1];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctl[C_TOTAL] = total;
-        if (total > cap)
-            ctl[C_BAD] = 1;
+    const uint32_t g = blockIdx.x * kT + threadIdx.x;
+    if (g < B.nb) {
+        const uint32_t no = B.m[g].no, base = osum[no] - tot[no];
+        const uint32_t total = osum[no + 2 * B.m[g].z + 2] - base;
+        ctl[C_TOTB + g] = total;
+        ctl[C_BASEB + g] = base;
+        if (total > B.m[g].cap)
+            ctl[C_BADB + g] = 1;
     }
-    if (total > cap)
-        return;
-    for (uint32_t id = blockIdx.x * kT + threadIdx.x; id < N; id += gridDim.x * kT) {
-        if (id < END && mark[id] && tot[id]) {
-            const uint32_t o = osum[id] - tot[id];   // output position
+    for (uint32_t id = g; id < B.N; id += gridDim.x * kT) {
+        const uint32_t b = blk_of_node(B, id), no = B.m[b].no;
+        if (id - no < 2 * B.m[b].z + 1 && mark[id] && tot[id]) {
+            const uint32_t o = osum[id] - tot[id] - (osum[no] - tot[no]);   // output position
             const uint4 f = fld[id];
             if (f.x && f.y > o)
-                ctl[C_BAD] = 1;                  // look-behind (lib/minilzo.c TEST_LB)
-            cover[o] = id;
+                ctl[C_BADB + b] = 1;             // look-behind (lib/minilzo.c TEST_LB)
+            if (o < B.m[b].cap)
+                cover[B.m[b].oo + o] = id;
         }
     }
 }
 
-__global__ __launch_bounds__(kT) void lat_origins(const uint32_t* __restrict__ cover, const uint32_t* __restrict__ tiles,
-                                                  const uint4* __restrict__ fld,
+__global__ __launch_bounds__(kT) void lat_origins(const Blks B, const uint32_t* __restrict__ cover,
+                                                  const uint32_t* __restrict__ tiles, const uint4* __restrict__ fld,
                                                   const uint32_t* __restrict__ tot, const uint32_t* __restrict__ osum,
                                                   uint32_t* __restrict__ org, const uint32_t* __restrict__ ctl)
 {
-    if (ctl[C_BAD])
-        return;
-    const uint32_t total = ctl[C_TOTAL];
-    for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < total; p += gridDim.x * kT) {
+    for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < B.C; p += gridDim.x * kT) {
+        const uint32_t b = blk_of_out(B, p), pl = p - B.m[b].oo;
+        if (ctl[C_BADB + b] || pl >= ctl[C_TOTB + b]) {
+            org[p] = kLitO;                      // (outside every block's output: never gathered)
+            continue;
+        }
         uint32_t id = cover[p];
         if (p >= kTile)
             id = umax32(tiles[p / kTile], id);   // (the cover scan's add pass)
         const uint4 f = fld[id];
-        const uint32_t o = osum[id] - tot[id];
-        const uint32_t r = p - o;
-        org[p] = r < f.x ? p - f.y : kLitO | (f.w + (r - f.x));
+        const uint32_t o = osum[id] - tot[id] - ctl[C_BASEB + b];
+        const uint32_t r = pl - o;
+        org[p] = r < f.x ? p - f.y : kLitO | (uint32_t)(B.m[b].in_off + f.w + (r - f.x));
     }
 }
 
 // one doubling round, in place (a partly updated source only shortens the
 // chain); a round after one that found nothing left returns at once
-__global__ __launch_bounds__(kT) void lat_double(uint32_t* org, uint32_t* __restrict__ ctl, uint32_t r)
+__global__ __launch_bounds__(kT) void lat_double(uint32_t* org, uint32_t C, uint32_t* __restrict__ ctl, uint32_t r)
 {
-    if (ctl[C_BAD] || (r > 0 && ctl[C_ROUND + r - 1] == 0))
+    if (r > 0 && ctl[C_ROUND + r - 1] == 0)
         return;
-    const uint32_t total = ctl[C_TOTAL];
     bool left = false;
-    for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < total; p += gridDim.x * kT) {
+    for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < C; p += gridDim.x * kT) {
         uint32_t o = __hip_atomic_load(org + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!(o & kLitO)) {
             // seven dereferences a pass: a chain shrinks 8x per launch
@@ -333,29 +378,32 @@ __global__ __launch_bounds__(kT) void lat_double(uint32_t* org, uint32_t* __rest
         ctl[C_ROUND + r] = 1;
 }
 
-__global__ __launch_bounds__(kT) void lat_gather(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                 const uint32_t* __restrict__ org, uint32_t* __restrict__ ctl,
+__global__ __launch_bounds__(kT) void lat_gather(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, const Blks B,
+                                                 const uint32_t* __restrict__ org, const uint32_t* __restrict__ ctl,
                                                  uint32_t* __restrict__ out_len, int32_t* __restrict__ status,
                                                  uint32_t* __restrict__ fallback, uint32_t* __restrict__ fallback_ids,
-                                                 uint32_t b, uint32_t rounds)
+                                                 uint32_t b0, uint32_t rounds)
 {
-    const bool bad = ctl[C_BAD] || ctl[C_ROUND + rounds - 1];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (bad) {
+    const bool stuck = ctl[C_ROUND + rounds - 1] != 0;   // (chains longer than the rounds: never on valid data)
+    const uint32_t g = blockIdx.x * kT + threadIdx.x;
+    if (g < B.nb) {
+        const uint32_t b = b0 + g;
+        if (ctl[C_BADB + g] || stuck) {
             out_len[b] = 0xFA110000u;
             status[b] = kFallback;
-            const uint32_t at = atomicAdd(&fallback[0], 1u);
-            fallback_ids[at] = b;
+            fallback_ids[atomicAdd(&fallback[0], 1u)] = b;
         } else {
-            out_len[b] = ctl[C_TOTAL];
+            out_len[b] = ctl[C_TOTB + g];
             status[b] = 0;
         }
     }
-    if (bad)
+    if (stuck)
         return;
-    const uint32_t total = ctl[C_TOTAL];
-    for (uint32_t p = blockIdx.x * kT + threadIdx.x; p < total; p += gridDim.x * kT)
-        out[p] = in[org[p] & ~kLitO];
+    for (uint32_t p = g; p < B.C; p += gridDim.x * kT) {
+        const uint32_t b = blk_of_out(B, p), pl = p - B.m[b].oo;
+        if (!ctl[C_BADB + b] && pl < ctl[C_TOTB + b])
+            dst[B.m[b].out_off + pl] = src[org[p] & ~kLitO];
+    }
 }
 
 // ---- scans (inclusive; MAX = running maximum, else running sum) -------------
@@ -469,9 +517,8 @@ struct Lay {
     size_t J, nst, mark, v, pmax, fld, tot, osum, tiles, ctl, cover, org, end;
 };
 
-Lay layout(uint32_t z, uint32_t cap)
+Lay layout(uint64_t N, uint64_t C, uint32_t K)
 {
-    const size_t N = 2 * (size_t)z + 3, K = levels_for(z);
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     Lay L;
     size_t o = 0;
@@ -484,42 +531,80 @@ Lay layout(uint32_t z, uint32_t cap)
     L.tot = o;   o = up(o + N * 4);
     L.osum = o;  o = up(o + N * 4);
     L.tiles = o; o = up(o + (size_t)kMaxTiles * 4);
-    L.ctl = o;   o = up(o + (C_ROUND + kRounds) * 4);
-    L.cover = o; o = up(o + (size_t)cap * 4);
-    L.org = o;   o = up(o + (size_t)cap * 4);
+    L.ctl = o;   o = up(o + C_WORDS * 4);
+    L.cover = o; o = up(o + C * 4);
+    L.org = o;   o = up(o + C * 4);
     L.end = o;
     return L;
 }
 
-}  // namespace
-
-static bool in_range(uint32_t z, uint32_t cap)
+// N, C and K of nb blocks, or false outside the decoder's range
+bool shape(const uint64_t* src_off, const uint32_t* z, const uint32_t* cap, uint32_t nb, uint64_t& N,
+           uint64_t& C, uint32_t& K)
 {
     const uint64_t lim = (uint64_t)kMaxTiles * kTile;   // elements one two-level scan takes
-    return z != 0 && cap != 0 && (uint64_t)2 * z + 3 <= lim && (uint64_t)cap <= lim;
+    if (nb == 0 || nb > kMaxBlk)
+        return false;
+    N = C = 0;
+    uint32_t zmax = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        if (z[b] == 0 || cap[b] == 0 || src_off[b] + z[b] >= (1ull << 31))
+            return false;
+        N += 2 * (uint64_t)z[b] + 3;
+        C += cap[b];
+        zmax = z[b] > zmax ? z[b] : zmax;
+    }
+    K = levels_for(zmax);
+    return N <= lim && C <= lim;
 }
 
-// 0: the block is outside the decoder's range (empty input or room, or more
-// than the scans take)
+}  // namespace
+
+// Scratch for nb <= 8 blocks decoded by one pipeline (host arrays); 0 when
+// they are outside the decoder's range (an empty input or room, more than 8
+// blocks, more than 16 Mi nodes or output slots).
+extern "C" size_t lzo_mi355x_decompress_lat_scratch_n(const uint64_t* src_off, const uint32_t* z,
+                                                      const uint32_t* cap, uint32_t nb)
+{
+    uint64_t N, C;
+    uint32_t K;
+    return shape(src_off, z, cap, nb, N, C, K) ? layout(N, C, K).end : 0;
+}
+
 extern "C" size_t lzo_mi355x_decompress_lat_scratch(uint32_t z, uint32_t cap)
 {
-    return in_range(z, cap) ? layout(z, cap).end : 0;
+    const uint64_t off = 0;
+    return lzo_mi355x_decompress_lat_scratch_n(&off, &z, &cap, 1);
 }
 
-// One block: in (z bytes) -> out (capacity cap); out_len[b] / status[b] as the
-// other decoders (0, or 0x7FFF0001 with b appended to the fallback list).
-extern "C" int lzo_mi355x_launch_decompress_lat(const uint8_t* in, uint32_t z, uint8_t* out, uint32_t cap,
-                                                uint32_t* out_len, int32_t* status, uint32_t* fallback,
-                                                uint32_t* fallback_ids, uint32_t b, void* scratch,
-                                                size_t scratch_bytes, hipStream_t s)
+// nb <= 8 blocks side by side: block b's z[b] bytes at src + src_off[b] into
+// dst + dst_off[b] (capacity cap[b]); out_len / status / fallback entries at
+// b0 + b (host arrays; src_off[b] + z[b] < 2^31).
+extern "C" int lzo_mi355x_launch_decompress_lat_n(const uint8_t* src, const uint64_t* src_off, const uint32_t* z,
+                                                  uint8_t* dst, const uint64_t* dst_off, const uint32_t* cap,
+                                                  uint32_t nb, uint32_t* out_len, int32_t* status,
+                                                  uint32_t* fallback, uint32_t* fallback_ids, uint32_t b0,
+                                                  void* scratch, size_t scratch_bytes, hipStream_t s)
 {
-    if (!in_range(z, cap))
+    uint64_t N64, C64;
+    uint32_t K;
+    if (!shape(src_off, z, cap, nb, N64, C64, K))
         return -1;
-    const Lay L = layout(z, cap);
+    const Lay L = layout(N64, C64, K);
     if (L.end > scratch_bytes)
         return -1;
+    const uint32_t N = (uint32_t)N64, C = (uint32_t)C64;
+    Blks B{};
+    B.nb = nb;
+    B.N = N;
+    B.C = C;
+    uint32_t no = 0, oo = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        B.m[b] = BlkMeta{no, z[b], oo, cap[b], src_off[b], dst_off[b]};
+        no += 2 * z[b] + 3;
+        oo += cap[b];
+    }
     uint8_t* S = (uint8_t*)scratch;
-    const uint32_t N = 2 * z + 3, K = levels_for(z);
     uint32_t* J = (uint32_t*)(S + L.J);
     uint32_t* nst = (uint32_t*)(S + L.nst);
     uint32_t* mark = (uint32_t*)(S + L.mark);
@@ -533,8 +618,8 @@ extern "C" int lzo_mi355x_launch_decompress_lat(const uint8_t* in, uint32_t z, u
     uint32_t* cover = (uint32_t*)(S + L.cover);
     uint32_t* org = (uint32_t*)(S + L.org);
     auto grid = [](uint32_t n) { uint32_t g = (n + kT - 1) / kT; return g < 1 ? 1u : (g > 4096u ? 4096u : g); };
-    const uint32_t gN = grid(N), gC = grid(cap);
-    hipLaunchKernelGGL(lat_nodes, dim3(gN > gC ? gN : gC), dim3(kT), 0, s, in, z, J, nst, mark, ctl, cover, cap);
+    const uint32_t gN = grid(N), gC = grid(C);
+    hipLaunchKernelGGL(lat_nodes, dim3(gN > gC ? gN : gC), dim3(kT), 0, s, src, B, J, nst, mark, ctl, cover);
     for (uint32_t k = 0; k + 1 < K; k += 3) {
         const uint32_t nl = K - 1 - k < 3 ? K - 1 - k : 3u;
         hipLaunchKernelGGL(lat_jump, dim3(gN), dim3(kT), 0, s, (const uint32_t*)(J + (size_t)k * N),
@@ -545,27 +630,41 @@ extern "C" int lzo_mi355x_launch_decompress_lat(const uint8_t* in, uint32_t z, u
         hipLaunchKernelGGL(lat_mark, dim3(gN), dim3(kT), 0, s, (const uint32_t*)J, mark, N, top - 1, nl);
         top -= nl;
     }
-    hipLaunchKernelGGL(lat_pred_in, dim3(gN), dim3(kT), 0, s, (const uint32_t*)mark, v, z, ctl);
+    hipLaunchKernelGGL(lat_pred_in, dim3(gN), dim3(kT), 0, s, B, (const uint32_t*)mark, v, ctl);
     if (scan<true>(v, pmax, N, tiles, gN, s) != 0)
         return -1;
-    hipLaunchKernelGGL(lat_fields, dim3(gN), dim3(kT), 0, s, in, z, (const uint32_t*)mark, (const uint32_t*)pmax,
+    hipLaunchKernelGGL(lat_fields, dim3(gN), dim3(kT), 0, s, src, B, (const uint32_t*)mark, (const uint32_t*)pmax,
                        (const uint32_t*)nst, fld, tot, ctl);
     if (scan<false>(tot, osum, N, tiles, gN, s) != 0)
         return -1;
-    hipLaunchKernelGGL(lat_starts, dim3(gN), dim3(kT), 0, s, (const uint32_t*)mark, (const uint4*)fld,
-                       (const uint32_t*)tot, (const uint32_t*)osum, z, cap, cover, ctl);
-    if (scan<true>(cover, cover, cap, tiles, gC, s, false) != 0)
+    hipLaunchKernelGGL(lat_starts, dim3(gN), dim3(kT), 0, s, B, (const uint32_t*)mark, (const uint4*)fld,
+                       (const uint32_t*)tot, (const uint32_t*)osum, cover, ctl);
+    if (scan<true>(cover, cover, C, tiles, gC, s, false) != 0)
         return -1;
-    hipLaunchKernelGGL(lat_origins, dim3(gC), dim3(kT), 0, s, (const uint32_t*)cover, (const uint32_t*)tiles,
-                       (const uint4*)fld,
-                       (const uint32_t*)tot, (const uint32_t*)osum, org, (const uint32_t*)ctl);
-    // chains are shorter than cap: 8^R > cap rounds at most
+    hipLaunchKernelGGL(lat_origins, dim3(gC), dim3(kT), 0, s, B, (const uint32_t*)cover, (const uint32_t*)tiles,
+                       (const uint4*)fld, (const uint32_t*)tot, (const uint32_t*)osum, org, (const uint32_t*)ctl);
+    // chains are shorter than any block's room: 8^R > the largest cap
+    uint32_t cmax = 0;
+    for (uint32_t b = 0; b < nb; b++)
+        cmax = cap[b] > cmax ? cap[b] : cmax;
     uint32_t R = 1;
-    while (R < kRounds && (1ull << (3 * R)) <= (uint64_t)cap)
+    while (R < kRounds && (1ull << (3 * R)) <= (uint64_t)cmax)
         R++;
     for (uint32_t r = 0; r < R; r++)
-        hipLaunchKernelGGL(lat_double, dim3(gC), dim3(kT), 0, s, org, ctl, r);
-    hipLaunchKernelGGL(lat_gather, dim3(gC), dim3(kT), 0, s, in, out, (const uint32_t*)org, ctl, out_len, status,
-                       fallback, fallback_ids, b, R);
+        hipLaunchKernelGGL(lat_double, dim3(gC), dim3(kT), 0, s, org, C, ctl, r);
+    hipLaunchKernelGGL(lat_gather, dim3(gC), dim3(kT), 0, s, src, dst, B, (const uint32_t*)org, (const uint32_t*)ctl,
+                       out_len, status, fallback, fallback_ids, b0, R);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// One block (the single-call path): out_len[b] / status[b] and the fallback
+// list as the other decoders (0, or 0x7FFF0001 with b appended).
+extern "C" int lzo_mi355x_launch_decompress_lat(const uint8_t* in, uint32_t z, uint8_t* out, uint32_t cap,
+                                                uint32_t* out_len, int32_t* status, uint32_t* fallback,
+                                                uint32_t* fallback_ids, uint32_t b, void* scratch,
+                                                size_t scratch_bytes, hipStream_t s)
+{
+    const uint64_t off = 0;
+    return lzo_mi355x_launch_decompress_lat_n(in, &off, &z, out, &off, &cap, 1, out_len, status, fallback,
+                                              fallback_ids, b, scratch, scratch_bytes, s);
 }

@@ -68,14 +68,8 @@ struct slot {
     size_t dcap;
     uint8_t *hmem;
     size_t hcap;
-    /* single calls: the latency decoder's scratch and streams (lane 0 runs on
-     * stream; lanes 1.. on their own streams, so that a group's blocks run
-     * their pipelines side by side) */
-    void *lat[4];
-    size_t latcap[4];
-    hipStream_t lst[4];
-    hipEvent_t lev[4];
-    int lready;
+    void *lat;                  /* single calls: the latency decoder's scratch */
+    size_t latcap;
 };
 
 /* A host thread's resources on one device: kSlots slots, so that several
@@ -112,16 +106,8 @@ static void tctx_free(void *p)
                 hipFree(c->s[k].dmem);
             if (c->s[k].hmem)
                 hipHostFree(c->s[k].hmem);
-            for (int j = 0; j < 4; j++) {
-                if (c->s[k].lat[j])
-                    hipFree(c->s[k].lat[j]);
-                if (j && (c->s[k].lready >> j) & 1) {
-                    hipStreamDestroy(c->s[k].lst[j]);
-                    hipEventDestroy(c->s[k].lev[j]);
-                }
-            }
-            if (c->s[k].lready & 1)
-                hipEventDestroy(c->s[k].lev[0]);
+            if (c->s[k].lat)
+                hipFree(c->s[k].lat);
             hipStreamDestroy(c->s[k].stream);
         }
     }
@@ -1037,9 +1023,10 @@ static struct slot *sc_slot(struct sc_queue *q)
 /* A decode whose compressed block is at least this long takes the latency
  * decoder (lzo1x_decode_lat.hip: the whole GPU on one block, 0.11-0.14 ms from
  * 32 KiB up to 536 KB, where the windowed decoder's one workgroup takes
- * 0.14-2.2 ms); shorter ones (equal at 12 KB) and combined groups the
- * windowed decoder (see lat_group).  POM_SC_LAT_MIN sets the threshold (bytes
- * of compressed input), POM_SC_LAT=0 turns it off. */
+ * 0.14-2.2 ms); shorter ones (equal at 12 KB) the windowed decoder, and so
+ * does a combined group with any such call or more than 8 calls (see
+ * lat_group).  POM_SC_LAT_MIN sets the threshold (bytes of compressed input),
+ * POM_SC_LAT=0 turns it off. */
 static int use_lat_decoder(size_t z)
 {
     static long min_z = -1;
@@ -1051,49 +1038,38 @@ static int use_lat_decoder(size_t z)
     return z >= (size_t)min_z;
 }
 
-/* the latency decoder's scratch per lane at most (a block needing more, from
- * ~4 MB of compressed input, takes the windowed decoder) */
+/* the latency decoder's scratch at most (a group needing more, from ~4 MB of
+ * compressed input, takes the windowed decoder) */
 static const size_t kLatMaxScratch = (size_t)1 << 30;
 
-enum { kLatLanes = 4 };
-
-/* Lane j of the slot's latency-decoder lanes: scratch of at least `bytes`,
- * and (j > 0) its stream and event.  Called only between groups, when no
- * pipeline of the slot is running. */
-static int lat_lane(struct slot *t, int j, size_t bytes)
+/* The slot's latency-decoder scratch, at least `bytes`.  Called only between
+ * groups, when nothing of the slot is running. */
+static int lat_reserve(struct slot *t, size_t bytes)
 {
-    if (!((t->lready >> j) & 1)) {
-        if (j && hipStreamCreateWithFlags(&t->lst[j], hipStreamNonBlocking) != hipSuccess)
-            return -1;
-        if (hipEventCreateWithFlags(&t->lev[j], hipEventDisableTiming) != hipSuccess)
-            return -1;
-        t->lready |= 1 << j;
-    }
-    if (t->latcap[j] >= bytes)
+    if (t->latcap >= bytes)
         return 0;
-    if (t->lat[j]) {
+    if (t->lat) {
         hipStreamSynchronize(t->stream);
-        hipFree(t->lat[j]);
-        t->lat[j] = NULL;
-        t->latcap[j] = 0;
+        hipFree(t->lat);
+        t->lat = NULL;
+        t->latcap = 0;
     }
     const size_t want = ALIGN_UP(bytes + bytes / 4, (size_t)1 << 20);
-    if (hipMalloc(&t->lat[j], want) != hipSuccess) {
-        t->lat[j] = NULL;
+    if (hipMalloc(&t->lat, want) != hipSuccess) {
+        t->lat = NULL;
         return -1;
     }
-    t->latcap[j] = want;
+    t->latcap = want;
     return 0;
 }
 
-/* The latency decoder for a group of k <= kLatGroup decodes, block i on lane
- * i mod kLatLanes, the lanes side by side after the input copy on s.
- * Returns 1 when launched, 0 when the group does not qualify (nothing
- * launched), -1 on a launch error.  Measured, pipelines on separate streams
- * do not overlap: a group of three 64 KiB blocks took 0.38 ms against 0.19
- * for one, and 8 calling threads got 7.8K calls/s against 11.3K with the
- * windowed decoder (one launch for the group).  So only lone calls take it. */
-enum { kLatGroup = 1 };
+/* A group of k <= 8 decodes of at least POM_SC_LAT_MIN compressed bytes each
+ * runs as ONE latency-decoder pipeline (lzo1x_decode_lat.hip: the blocks side
+ * by side in every kernel).  Returns 1 when launched, 0 when the group does
+ * not qualify (nothing launched), -1 on a launch error.  (Separate pipelines
+ * on four streams were measured first: they did not overlap -- three 64 KiB
+ * blocks 0.38 ms against 0.19 for one.) */
+enum { kLatGroup = 8 };
 
 static int lat_group(struct slot *t, struct sc_req **g, int k, const uint8_t *d, uint8_t *out,
                      const size_t *o_src, const size_t *o_out, uint32_t *olen, int32_t *ost, uint32_t *fb,
@@ -1101,39 +1077,21 @@ static int lat_group(struct slot *t, struct sc_req **g, int k, const uint8_t *d,
 {
     if (k > kLatGroup)
         return 0;
-    const int nl = k < kLatLanes ? k : kLatLanes;
-    size_t need[kLatLanes] = {0};
+    uint64_t so[kLatGroup], doff[kLatGroup];
+    uint32_t z[kLatGroup], cap[kLatGroup];
     for (int i = 0; i < k; i++) {
         if (!use_lat_decoder(g[i]->src_len) || g[i]->room > 0xFFFFFFFFu)
             return 0;
-        const size_t n = lzo_mi355x_decompress_lat_scratch((uint32_t)g[i]->src_len, (uint32_t)g[i]->room);
-        if (n == 0 || n > kLatMaxScratch)
-            return 0;                           /* out of its range: the windowed decoder */
-        if (n > need[i % nl])
-            need[i % nl] = n;
+        so[i] = o_src[i];
+        doff[i] = o_out[i];
+        z[i] = (uint32_t)g[i]->src_len;
+        cap[i] = (uint32_t)g[i]->room;
     }
-    for (int j = 0; j < nl; j++)
-        if (lat_lane(t, j, need[j]) != 0)
-            return 0;
-    if (nl > 1) {
-        if (hipEventRecord(t->lev[0], s) != hipSuccess)
-            return -1;
-        for (int j = 1; j < nl; j++)
-            if (hipStreamWaitEvent(t->lst[j], t->lev[0], 0) != hipSuccess)
-                return -1;
-    }
-    for (int i = 0; i < k; i++) {
-        const int j = i % nl;
-        if (lzo_mi355x_launch_decompress_lat(d + o_src[i], (uint32_t)g[i]->src_len, out + o_out[i],
-                                             (uint32_t)g[i]->room, olen, ost, fb, fb + 1, (uint32_t)i,
-                                             t->lat[j], t->latcap[j], j ? t->lst[j] : s) != 0)
-            return -1;
-    }
-    for (int j = 1; j < nl; j++)
-        if (hipEventRecord(t->lev[j], t->lst[j]) != hipSuccess ||
-            hipStreamWaitEvent(s, t->lev[j], 0) != hipSuccess)
-            return -1;
-    return 1;
+    const size_t need = lzo_mi355x_decompress_lat_scratch_n(so, z, cap, (uint32_t)k);
+    if (need == 0 || need > kLatMaxScratch || lat_reserve(t, need) != 0)
+        return 0;                               /* out of its range: the windowed decoder */
+    return lzo_mi355x_launch_decompress_lat_n(d, so, z, out, doff, cap, (uint32_t)k, olen, ost, fb, fb + 1, 0,
+                                              t->lat, t->latcap, s) == 0 ? 1 : -1;
 }
 
 static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)

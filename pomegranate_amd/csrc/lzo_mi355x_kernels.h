@@ -110,6 +110,18 @@ int lzo_mi355x_launch_decompress_lat(const uint8_t *in, uint32_t z, uint8_t *out
                                      uint32_t *fallback_ids, uint32_t b, void *scratch,
                                      size_t scratch_bytes, hipStream_t stream);
 
+/* Up to 8 blocks side by side in one latency-decoder pipeline (host arrays:
+ * block b is z[b] bytes at src + src_off[b] into dst + dst_off[b], capacity
+ * cap[b]; results at b0 + b; src_off[b] + z[b] < 2^31).  Scratch 0: outside
+ * the range. */
+size_t lzo_mi355x_decompress_lat_scratch_n(const uint64_t *src_off, const uint32_t *z, const uint32_t *cap,
+                                           uint32_t nb);
+int lzo_mi355x_launch_decompress_lat_n(const uint8_t *src, const uint64_t *src_off, const uint32_t *z,
+                                       uint8_t *dst, const uint64_t *dst_off, const uint32_t *cap, uint32_t nb,
+                                       uint32_t *out_len, int32_t *status, uint32_t *fallback,
+                                       uint32_t *fallback_ids, uint32_t b0, void *scratch, size_t scratch_bytes,
+                                       hipStream_t stream);
+
 /* Unchecked-decoder pre-scan: decoded length and status per block; with
  * cap_out, also min(length, cap_limit) per block (a decode's capacity). */
 int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off,

@@ -117,21 +117,30 @@ def gpu_decompress_win(torch, comps: Sequence[bytes], caps: Sequence[int], dev, 
     return fetch(dst, olen, cap=caps), st.cpu().numpy().tolist(), sorted(ids[:nfb].cpu().numpy().tolist())
 
 
-def gpu_decompress_lat(torch, comps: Sequence[bytes], caps: Sequence[int], dev):
-    """The latency decoder (lzo_mi355x_launch_decompress_lat) alone, one block
-    per pipeline, without the exact decoder behind it.  Returns the outputs,
-    statuses and the ids of the blocks it handed over; a block outside its
-    range (the launcher returns -1) is reported with status None."""
+def gpu_decompress_lat(torch, comps: Sequence[bytes], caps: Sequence[int], dev, group: int = 1):
+    """The latency decoder (lzo1x_decode_lat.hip) alone, without the exact
+    decoder behind it: one block per pipeline (group 1,
+    lzo_mi355x_launch_decompress_lat) or up to `group` blocks side by side in
+    one pipeline (lzo_mi355x_launch_decompress_lat_n).  Returns the outputs,
+    statuses and the ids of the blocks it handed over; blocks outside its range
+    (the launcher returns -1) are reported with status None."""
     import ctypes
     lib = lzo.load()
-    fn = lib.lzo_mi355x_launch_decompress_lat
-    fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
-                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    one = lib.lzo_mi355x_launch_decompress_lat
+    one.restype = ctypes.c_int
+    one.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    many = lib.lzo_mi355x_launch_decompress_lat_n
+    many.restype = ctypes.c_int
+    many.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4 + \
+        [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     sz = lib.lzo_mi355x_decompress_lat_scratch
     sz.restype = ctypes.c_size_t
     sz.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    szn = lib.lzo_mi355x_decompress_lat_scratch_n
+    szn.restype = ctypes.c_size_t
+    szn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
     src = device_batch(torch, comps, dev)
     dst = empty_batch(torch, caps, dev, fill=0x5A)
     n = len(comps)
@@ -141,16 +150,30 @@ def gpu_decompress_lat(torch, comps: Sequence[bytes], caps: Sequence[int], dev):
     ids = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
     p = lambda x: x.data_ptr()
     s = torch.cuda.current_stream().cuda_stream
-    soff = src.off.cpu().numpy()
-    doff = dst.off.cpu().numpy()
-    launched = []
-    for i, (z, cap) in enumerate(zip(comps, caps)):
-        need = int(sz(len(z), int(cap))) if len(z) else 0
-        scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
-        rc = fn(p(src.arena) + int(soff[i]), len(z), p(dst.arena) + int(doff[i]), int(cap),
-                p(olen), p(st), p(head), p(ids), i, p(scratch), need, s)
+    soff = src.off.cpu().numpy().astype(np.uint64)
+    doff = dst.off.cpu().numpy().astype(np.uint64)
+    launched = [False] * n
+    for g0 in range(0, n, group):
+        g1 = min(n, g0 + group)
+        if group == 1:
+            z, cap = comps[g0], int(caps[g0])
+            need = int(sz(len(z), cap)) if len(z) else 0
+            scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+            rc = one(p(src.arena) + int(soff[g0]), len(z), p(dst.arena) + int(doff[g0]), cap,
+                     p(olen), p(st), p(head), p(ids), g0, p(scratch), need, s)
+        else:
+            so = np.ascontiguousarray(soff[g0:g1] - soff[g0])
+            do = np.ascontiguousarray(doff[g0:g1] - doff[g0])
+            zz = np.array([len(c) for c in comps[g0:g1]], dtype=np.uint32)
+            cc = np.array([int(c) for c in caps[g0:g1]], dtype=np.uint32)
+            need = int(szn(so.ctypes.data, zz.ctypes.data, cc.ctypes.data, g1 - g0))
+            scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+            rc = many(p(src.arena) + int(soff[g0]), so.ctypes.data, zz.ctypes.data,
+                      p(dst.arena) + int(doff[g0]), do.ctypes.data, cc.ctypes.data, g1 - g0,
+                      p(olen), p(st), p(head), p(ids), g0, p(scratch), need, s)
         torch.cuda.synchronize()
-        launched.append(rc == 0)
+        for i in range(g0, g1):
+            launched[i] = rc == 0
     nfb = int(head[0].item())
     sts = [x if ok else None for x, ok in zip(st.cpu().numpy().tolist(), launched)]
     return fetch(dst, olen, cap=caps), sts, sorted(ids[:nfb].cpu().numpy().tolist())

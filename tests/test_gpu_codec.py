@@ -704,9 +704,10 @@ def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, kind, malfo
     assert handed2 == [0, 1, 2, 3] and st2 == [0x7FFF0001] * 4
 
 
-def test_latency_decoder_valid_streams(dev, gu):
+@pytest.mark.parametrize("group", [1, 8])
+def test_latency_decoder_valid_streams(dev, gu, group):
     """The latency decoder (lzo1x_decode_lat.hip) alone, one block per
-    pipeline: every content model, ITB blocks up to the 536,192-byte maximum, a
+    pipeline and eight side by side: every content model, ITB blocks up to the 536,192-byte maximum, a
     1 MiB block and the full-grammar streams (M1 after runs and trailing
     literals, long extensions, first runs of 1-3 bytes) decode bit-exactly,
     none handed over."""
@@ -721,21 +722,22 @@ def test_latency_decoder_valid_streams(dev, gu):
     streams = [lzo_streams.stream(2100 + s, [50, 300, 5000, 40000, 150000][s % 5]) for s in range(20)]
     comps += [z for z, _ in streams]
     want = blocks + [o for _, o in streams]
-    outs, st2, handed = gu.gpu_decompress_lat(torch, comps, [len(w) for w in want], dev)
+    outs, st2, handed = gu.gpu_decompress_lat(torch, comps, [len(w) for w in want], dev, group)
     assert handed == []
     assert st2 == [0] * len(want)
     bad = [i for i, (o, w) in enumerate(zip(outs, want)) if o != w]
     assert not bad, bad[:8]
 
 
-def test_latency_decoder_hands_over_malformed_and_short_room(dev, gu, malformed):
+@pytest.mark.parametrize("group", [1, 8])
+def test_latency_decoder_hands_over_malformed_and_short_room(dev, gu, malformed, group):
     """Malformed streams, and valid streams whose output does not fit, are
     handed to the exact decoder (status 0x7FFF0001) -- never reported OK with
     wrong bytes."""
     comps = list(malformed["streams"][:200])
     caps = list(malformed["caps"][:200])
     want_codes = list(malformed["rc"][:200])
-    outs, st, handed = gu.gpu_decompress_lat(torch, comps, caps, dev)
+    outs, st, handed = gu.gpu_decompress_lat(torch, comps, caps, dev, group)
     for i, (s, code) in enumerate(zip(st, want_codes)):
         if s is None:                            # outside the decoder's range: not launched
             continue
@@ -745,7 +747,7 @@ def test_latency_decoder_hands_over_malformed_and_short_room(dev, gu, malformed)
             assert s == 0x7FFF0001 and i in handed
     blocks = [synth.block(synth.ITB, 9200 + i, 65536) for i in range(3)]
     comps2, _ = gu.gpu_compress(torch, blocks, dev)
-    outs2, st2, handed2 = gu.gpu_decompress_lat(torch, comps2, [65535] * 3, dev)
+    outs2, st2, handed2 = gu.gpu_decompress_lat(torch, comps2, [65535] * 3, dev, group)
     assert handed2 == [0, 1, 2] and st2 == [0x7FFF0001] * 3
 
 
