@@ -568,6 +568,47 @@ static double now_ms(void)
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
+/* the latency decoder's scratch at most (a group needing more, from ~4 MB of
+ * compressed input, takes the windowed decoder) */
+static const size_t kLatMaxScratch = (size_t)1 << 30;
+static int use_lat_decoder(size_t z);
+static int lat_reserve(struct slot *t, size_t bytes);
+
+/* A decompress chunk of at most 8 blocks, each of at least POM_SC_LAT_MIN
+ * compressed bytes, decodes on one latency-decoder pipeline (the whole GPU on
+ * these few blocks; lzo1x_decode_lat.hip) with the exact decoder behind it for
+ * the blocks it hands over.  1 launched, 0 not eligible (nothing launched),
+ * -1 on an error. */
+static int lat_chunk(struct slot *S, const struct layout *L, const uint8_t *h, uint8_t *d, hipStream_t s)
+{
+    const uint32_t nb = (uint32_t)L->nb;
+    if (nb == 0 || nb > 8)
+        return 0;
+    const uint64_t *so = (const uint64_t *)(h + L->o_srcoff);
+    const uint64_t *dof = (const uint64_t *)(h + L->o_dstoff);
+    const uint32_t *sl = (const uint32_t *)(h + L->o_srclen);
+    const uint32_t *dc = (const uint32_t *)(h + L->o_dstcap);
+    for (uint32_t i = 0; i < nb; i++)
+        if (!use_lat_decoder(sl[i]))
+            return 0;
+    const size_t need = lzo_mi355x_decompress_lat_scratch_n(so, sl, dc, nb);
+    if (need == 0 || need > kLatMaxScratch || lat_reserve(S, need) != 0)
+        return 0;
+    uint8_t *scr = d + L->o_scr;
+    uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nb));
+    uint32_t *ol = (uint32_t *)(d + L->o_outlen);
+    int32_t *st = (int32_t *)(d + L->o_status);
+    if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess ||
+        lzo_mi355x_launch_decompress_lat_n(d + L->o_src, so, sl, d + L->o_dst, dof, dc, nb, ol, st, fb, ids, 0,
+                                           S->lat, S->latcap, s) != 0 ||
+        lzo_mi355x_launch_decompress_exact(d + L->o_src, (const uint64_t *)(d + L->o_srcoff),
+                                           (const uint32_t *)(d + L->o_srclen), d + L->o_dst,
+                                           (const uint64_t *)(d + L->o_dstoff), (const uint32_t *)(d + L->o_dstcap),
+                                           ol, st, fb, ids, nb, nb, 0, s) != 0)
+        return -1;
+    return 1;
+}
+
 /* Chunk on slot S: inputs into pinned staging, H2D, kernels, D2H of the
  * lengths -- all queued on the slot's stream, nothing waited for. */
 static int chunk_launch(struct slot *S, struct layout *L, const struct hbatch *B)
@@ -595,8 +636,10 @@ static int chunk_launch(struct slot *S, struct layout *L, const struct hbatch *B
     if (B->kind == OP_COMPRESS)
         rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb,
                                      nb <= B->enc_lds_max ? NULL : d + L->o_scr, s);
-    else if (B->kind == OP_DECOMPRESS)
-        rc = decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, 0, s);
+    else if (B->kind == OP_DECOMPRESS) {
+        const int lat = lat_chunk(S, L, h, d, s);
+        rc = lat < 0 ? -1 : lat > 0 ? 0 : decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, 0, s);
+    }
     else
         rc = lzo_mi355x_launch_decompress_concat(dsrc, so, sl, ddst, dof, dc, ol, st, nb, s);
     if (rc != 0)
@@ -1038,9 +1081,6 @@ static int use_lat_decoder(size_t z)
     return z >= (size_t)min_z;
 }
 
-/* the latency decoder's scratch at most (a group needing more, from ~4 MB of
- * compressed input, takes the windowed decoder) */
-static const size_t kLatMaxScratch = (size_t)1 << 30;
 
 /* The slot's latency-decoder scratch, at least `bytes`.  Called only between
  * groups, when nothing of the slot is running. */

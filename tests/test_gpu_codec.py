@@ -772,3 +772,30 @@ def test_lone_single_calls_on_the_latency_decoder(dev, oracle):
         cut = z[: len(z) // 2]
         rc, _ = lzo.lzo1x_decompress_safe(cut, n)
         assert rc == oracle.decompress_safe(cut, n)[0]
+
+
+@pytest.mark.parametrize("k", [1, 3, 8])
+def test_small_host_batches_on_the_latency_decoder(dev, oracle, malformed, k):
+    """Host batches of up to 8 blocks of 2 KB or more of compressed input
+    decode on one latency-decoder pipeline (lzo_host.c lat_chunk) with the
+    exact decoder behind it: exact bytes, a block one byte short of room
+    (OUTPUT_OVERRUN) and a malformed stream's reference code in the same
+    batch."""
+    blocks = [synth.block(synth.ITB if i % 2 else synth.TEXT, 6161 + i, 20000 + 9000 * i) for i in range(k)]
+    comps = [oracle.compress(b) for b in blocks]
+    assert all(len(z) >= 2048 for z in comps)
+    caps = [len(b) for b in blocks]
+    want = [(0, b) for b in blocks]
+    if k > 1:
+        caps[0] -= 1
+        want[0] = oracle.decompress_safe(comps[0], caps[0])
+    if k > 2:
+        j = next(i for i, z in enumerate(malformed["streams"]) if len(z) >= 2048 and malformed["rc"][i] != 0)
+        comps[1], caps[1] = malformed["streams"][j], int(malformed["caps"][j])
+        want[1] = oracle.decompress_safe(comps[1], caps[1])
+    rc, status, outs = lzo.decompress_batch(comps, caps)
+    assert rc == 0
+    for i, (s, o) in enumerate(zip(status, outs)):
+        assert s == want[i][0], (i, s, want[i][0])
+        if s == 0:
+            assert o == want[i][1], i
