@@ -1,8 +1,11 @@
-// lzo1x_decode_lat.hip -- the latency decoder for MI355X (gfx950): ONE block
-// decoded by the whole GPU as a pipeline of data-parallel kernels, with no
-// per-window chain.  For lone large blocks (single calls of
-// ITBs up to 536,192 B, include/xtable.h:136-144), where every throughput
-// decoder is one workgroup's serial chain.
+// lzo1x_decode_lat.hip -- the latency decoder for MI355X (gfx950): one block,
+// or up to 8 side by side, decoded by the whole GPU as a pipeline of
+// data-parallel kernels, with no per-window chain.  For single
+// calls and small batches of ITBs up to 536,192 B (include/xtable.h:136-144),
+// where every throughput decoder is one workgroup's serial chain.  With
+// several blocks every kernel runs over the flattened node and output spaces;
+// jumps, marks and origins never leave a block (END and BAD absorb, look-behind
+// is checked), and each element finds its block in the kernel argument.
 //
 // Grammar: lib/minilzo.c:3308-3699.  Stages:
 //  1. NODES: every (position, state class) of the compressed stream -- class
