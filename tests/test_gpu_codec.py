@@ -642,7 +642,7 @@ def test_encoder_block_tickets_mixed_sizes(dev, gu):
     assert torch.equal(back, src.arena)
 
 
-@pytest.mark.parametrize("kind", ["win", "ser", "row"])
+@pytest.mark.parametrize("kind", ["win", "ser", "row", "seg"])
 def test_window_decoder_every_valid_stream(dev, gu, kind):
     """The windowed (lzo1x_decode_win.hip) and table-walk
     (lzo1x_decode_ser.hip) decoders alone, without the exact decoder behind it: every content model (incompressible blocks with
@@ -668,7 +668,7 @@ def test_window_decoder_every_valid_stream(dev, gu, kind):
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("kind", ["win", "ser", "row"])
+@pytest.mark.parametrize("kind", ["win", "ser", "row", "seg"])
 def test_window_decoder_full_grammar_streams(dev, gu, kind):
     """LZO1X streams the LZO1X-1 compressor never writes (M1 after literal runs
     and trailing literals, long extensions, first runs of 1-3 bytes) decode
@@ -684,7 +684,7 @@ def test_window_decoder_full_grammar_streams(dev, gu, kind):
     assert outs == want
 
 
-@pytest.mark.parametrize("kind", ["win", "ser", "row"])
+@pytest.mark.parametrize("kind", ["win", "ser", "row", "seg"])
 def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, kind, malformed):
     """Malformed streams, and valid streams whose output does not fit, are
     handed to the exact decoder (status 0x7FFF0001 until it runs) -- never
