@@ -570,7 +570,7 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
         "roofline": roofline("decode", z_bytes + n_bytes, t_d, bb, nb,
                              "lzo1x_decode_fast_kernel (+ the exact pass over its refusals)"),
         "compress_roofline": roofline("encode", z_bytes + n_bytes, t_c, bb, nb,
-                                      "lzo1x_encode_gdict1_kernel" if os.environ.get("POM_ENC_WAVES", "1") == "1"
+                                      "lzo1x_encode_gdict1_kernel" if "enc_waves=2" not in os.environ.get("POM_LZO_DEBUG", "")
                                       else "lzo1x_encode_gdict_kernel"),
         "step_ms": {"compress": round(t_c * 1e3, 4), "decompress": round(t_d * 1e3, 4)},
         "decompress_gibps": round(dec_gibps, 3),

@@ -84,7 +84,7 @@ int lzo_mi355x_decoded_length(const uint8_t *src, unsigned long src_len,
  * xnet wire).  The blocks are ordered largest first and dealt round robin
  * over the GPUs (POM_LZO_DEVICES, default all; a batch below 64 MiB a GPU
  * stays on the caller's current GPU).  Each GPU's share is cut into chunks of
- * at most 128 MiB of input plus output capacity (POM_LZO_CHUNK_MB; the first
+ * at most 128 MiB of input plus output capacity (debug key chunk_mb of POM_LZO_DEBUG; the first
  * chunk a quarter of that), each packed into pinned staging, copied to the
  * GPU with hipMemcpyAsync, coded and copied back, up to four chunks in flight
  * on four streams, so staging stays bounded whatever the batch size.

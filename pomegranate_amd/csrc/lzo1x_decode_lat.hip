@@ -104,10 +104,15 @@ __device__ Ins decode_at(const uint8_t* in, uint32_t z, uint32_t p, uint32_t s)
     if (q >= z)
         return x;
     const uint32_t t = ib(in, z, q++);
+    // A length extension: zero bytes count 255 each.  Every node of a zero run
+    // would scan the rest of the run, so a node gives up after kExtMax zero
+    // bytes (a length past ~16 K): refused here, the block goes to the exact
+    // decoder, which decodes such a stream in linear time.
+    constexpr uint32_t kExtMax = 64;
     auto ext = [&](uint32_t base, uint32_t& n) -> bool {
         uint32_t v = 0;
         for (;;) {
-            if (q >= z || v > (1u << 24))
+            if (q >= z || v >= kExtMax * 255u)
                 return false;
             const uint32_t b = ib(in, z, q++);
             if (b) {

@@ -57,17 +57,30 @@ constexpr uint32_t kFarSpan = 3072;              // largest window output with f
 constexpr uint32_t kRoom = kRing - kChunk;       // unstored output the slow path lets the ring hold
 constexpr int32_t kFallback = 0x7FFF0001;
 
-// LDS: ring | stage | table (u16 [512] while parsing, u64 [128] descriptors
-// while executing) | row marks | trash (the target of masked-out lanes)
+#ifndef POM_SEG_ROWS
+#define POM_SEG_ROWS 4
+#endif
+constexpr int kRows = POM_SEG_ROWS;              // rows of 64 bytes per group
+constexpr uint32_t kGroup = kRows * kWave;       // output bytes per row group
+
+// LDS: ring | stage | jump table (u16 [512] while parsing; u64 [129] segment
+// descriptors while executing) | step table (u8 [512] while parsing; then 4
+// rows of marks and the trash, the target of masked-out lanes)
 constexpr uint32_t kStageOff = kRing;
-constexpr uint32_t kTabOff = kStageOff + kStage;
-constexpr uint32_t kTabBytes = 1024;
-constexpr uint32_t kMarkOff = kTabOff + kTabBytes;
-constexpr uint32_t kTrashOff = kMarkOff + kWave;
-constexpr uint32_t kLdsBytes = kTrashOff + kWave;
+constexpr uint32_t kJumpOff = kStageOff + kStage;
+constexpr uint32_t kJumpBytes = 1040;
+constexpr uint32_t kStepOff = kJumpOff + kJumpBytes;
+constexpr uint32_t kStepBytes = 512;
+constexpr uint32_t kMarkOff = kStepOff;
+constexpr uint32_t kTrashOff = kMarkOff + 4 * kWave;
+constexpr uint32_t kLdsBytes = kStepOff + kStepBytes;
 static_assert(kLdsBytes * 16 <= 160 * 1024, "16 blocks per CU");
-static_assert(kTabOff % 16 == 0, "descriptors: ds_write_b128");
-static_assert(2 * 2 * kPiece <= kTabBytes && 8 * 2 * kWave <= kTabBytes, "table overlay");
+static_assert(kJumpOff % 16 == 0 && kStepOff % 16 == 0, "table alignment");
+static_assert(2 * 2 * kPiece <= kJumpBytes && 8 * (2 * kWave + 1) <= kJumpBytes, "jump table / descriptors");
+static_assert(kTrashOff + kWave <= kStepOff + kStepBytes, "marks and trash over the step table");
+
+// jump entries: target node (10 bits) | steps taken (3 bits) | stopped
+constexpr uint32_t kJStop = 1u << 13;
 
 // exact instruction-start states
 constexpr uint32_t ST_A = 0;                     // top of the loop
@@ -75,8 +88,9 @@ constexpr uint32_t ST_B = 1;                     // after a literal run (t < 16:
 constexpr uint32_t ST_C = 2;                     // after 1-3 trailing literals (t < 16: 2-byte M1)
 constexpr uint32_t ST_F = 3;                     // first byte of the stream (lib/minilzo.c:3357)
 
-// descriptor flags (high word of a match segment's descriptor)
-constexpr uint32_t kPer = 1u << 30;              // d < L: the match repeats a period of d
+// descriptor flags (high word of a match segment's descriptor): d in bits
+// 0-15, or for kPerS d in bits 0-7 and floor(65536 / d) + 1 in bits 8-24
+constexpr uint32_t kPerS = 1u << 30;             // d < min(L, 256): repeats a period of d
 constexpr uint32_t kFar = 1u << 31;              // copied before the rows
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -226,12 +240,12 @@ __device__ __noinline__ Ins decode_slow(Src S, uint32_t p, uint32_t s)
     return x;
 }
 
-// Table entries of the instructions starting at piece position r with bytes
-// t b1 b2 b3, for class A (.x) and class N (.y): (next << 1 | next class) |
-// 0x8000 when the next start leaves the piece; 0 for a rare instruction or
-// one that ends past lim (the reach, or the input end).
-__device__ __forceinline__ uint2 table_pair(uint32_t t, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t r,
-                                            uint32_t lim)
+// Step entries of the instructions starting at piece position r with bytes
+// t b1 b2 b3, for class A (.x) and class N (.y): the instruction's length
+// with its literals (at most 63) | the next class << 6; 0 for a rare
+// instruction or one that ends past lim (the reach, or the input end).
+__device__ __forceinline__ uint2 step_pair(uint32_t t, uint32_t b1, uint32_t b2, uint32_t b3, uint32_t r,
+                                           uint32_t lim)
 {
     const bool lo = t < 16, m2 = t >= 64, m3 = t >= 32 && t < 64, m4 = t >= 16 && t < 32;
     const bool ext = (m3 && (t & 31) == 0) || (m4 && (t & 7) == 0);
@@ -239,14 +253,22 @@ __device__ __forceinline__ uint2 table_pair(uint32_t t, uint32_t b1, uint32_t b2
     const bool eof = m4 && (t & 8) == 0 && (w >> 2) == 0;
     const uint32_t ilen = (m2 || lo) ? 2u : (ext ? 4u : 3u);
     const uint32_t T = ((m2 || lo) ? t : w) & 3u;
-    const uint32_t nN = r + ilen + T;
-    const bool rN = (ext && b1 == 0) || eof || nN > lim;
-    const uint32_t eN = rN ? 0u : ((nN << 1) | (T ? 1u : 0u)) | (nN >= kPiece ? 0x8000u : 0u);
+    const uint32_t lN = ilen + T;
+    const bool rN = (ext && b1 == 0) || eof || r + lN > lim;
+    const uint32_t eN = rN ? 0u : lN | (T ? 0x40u : 0u);
     // class A, t < 16: a literal run of t + 3 (1-byte header) or 18 + b1 (2-byte header)
-    const uint32_t nR = r + (t ? t + 4u : 20u + b1);
-    const bool rR = (t == 0 && b1 == 0) || nR > lim;
-    const uint32_t eR = rR ? 0u : ((nR << 1) | 1u) | (nR >= kPiece ? 0x8000u : 0u);
+    const uint32_t lR = t ? t + 4u : 20u + b1;
+    const bool rR = (t == 0 && b1 == 0) || lR > 63 || r + lR > lim;
+    const uint32_t eR = rR ? 0u : lR | 0x40u;
     return make_uint2(lo ? eR : eN, eN);
+}
+
+// The jump entry of one step from node (r, c) with step entry e.
+__device__ __forceinline__ uint32_t jump1(uint32_t r, uint32_t e, uint32_t node)
+{
+    const uint32_t nr = r + (e & 63u);
+    const uint32_t tgt = (nr << 1) | (e >> 6);
+    return e == 0 ? (node | kJStop) : (tgt | (1u << 10) | (nr >= kPiece ? kJStop : 0u));
 }
 
 struct Out {
@@ -387,9 +409,10 @@ __device__ __forceinline__ void close_block(uint32_t b, bool ok, uint32_t len, u
 }
 
 // (diagnostics, STAMPS) per-phase s_memtime cycle sums, 16 x u64 per block:
-// 0 stage + table, 1 walk, 2 decode + checks, 3 far copies, 4 rows, 5 rare
-// instructions; counts: 8 windows, 9 instructions, 10 rows, 11 sub-passes,
-// 12 far batches, 13 rare instructions, 14 rows with starts
+// 0 stage + tables, 1 walk + expansion, 2 decode + checks, 3 far copies,
+// 4 rows, 5 rare instructions; counts: 8 windows, 9 instructions, 10 row
+// groups, 11 sub-passes, 12 far batches, 13 rare instructions, 14 groups with
+// segment starts
 template <bool STAMPS>
 __global__ __launch_bounds__(kWave, 4) void lzo1x_decode_seg_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
@@ -429,57 +452,104 @@ __global__ __launch_bounds__(kWave, 4) void lzo1x_decode_seg_kernel(
     }
     const Src S = make_src(src + src_off[b], z);
     const uint32_t trash = kTrashOff + l;
-    uint16_t* const tab16 = (uint16_t*)(lds + kTabOff);
+    const uint16_t* const jump = (const uint16_t*)(lds + kJumpOff);
 
     uint32_t p = 0, st = ST_F;                   // next instruction start and its exact state
     uint32_t op = 0;                             // output position
     bool ok = true;
+    // input words of piece pfP (lanes < kStage / 8): the next piece is loaded
+    // while the current window executes
+    uint32_t pfP = 0xFFFFFFFFu, pf0 = 0, pf1 = 0, pf2 = 0;
     for (;;) {
         uint32_t n = 0, cur = 0;
         bool rare = true;
-        uint32_t P = p & ~3u;
+        const uint32_t P = p & ~3u;
         if (st != ST_F) {
-            // ---- 1. piece: stage and table --------------------------------------
+            // ---- 1. piece: stage, step table, 4-step jump table -----------------
             if (l < kStage / 8) {
-                const uint32_t a = S.sh + P + 8 * l;    // (P and the piece are dword aligned)
-                const uint32_t a0 = a & ~3u;
-                const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0, 0, 0);
-                const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0 + 4, 0, 0);
-                const uint32_t w2 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0 + 8, 0, 0);
+                if (P != pfP) {
+                    const uint32_t a0 = (S.sh + P + 8 * l) & ~3u;   // (P is dword aligned)
+                    pf0 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0, 0, 0);
+                    pf1 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0 + 4, 0, 0);
+                    pf2 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0 + 8, 0, 0);
+                }
                 *(uint2*)(lds + kStageOff + 8 * l) =
-                    make_uint2(__builtin_amdgcn_alignbyte(w1, w0, S.sh), __builtin_amdgcn_alignbyte(w2, w1, S.sh));
+                    make_uint2(__builtin_amdgcn_alignbyte(pf1, pf0, S.sh), __builtin_amdgcn_alignbyte(pf2, pf1, S.sh));
             }
+            pfP = P;
             {
+                // lane l: nodes 8l .. 8l + 7 (positions 4l .. 4l + 3, both classes)
                 const uint32_t lim = z - P < kReach ? z - P : kReach;
                 const uint32_t d0 = *(const uint32_t*)(lds + kStageOff + 4 * l);
                 const uint32_t d1 = *(const uint32_t*)(lds + kStageOff + 4 * l + 4);
-                uint32_t e[4];
+                uint32_t e8[8], jv[8];
 #pragma unroll
                 for (uint32_t j = 0; j < 4; j++) {
                     const uint32_t w = __builtin_amdgcn_alignbyte(d1, d0, j);
-                    const uint2 tp = table_pair(w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF, w >> 24, 4 * l + j, lim);
-                    e[j] = tp.x | (tp.y << 16);
+                    const uint32_t r = 4 * l + j;
+                    const uint2 sp = step_pair(w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF, w >> 24, r, lim);
+                    e8[2 * j] = sp.x;
+                    e8[2 * j + 1] = sp.y;
+                    jv[2 * j] = jump1(r, sp.x, 2 * r);
+                    jv[2 * j + 1] = jump1(r, sp.y, 2 * r + 1);
                 }
-                *(uint4*)(lds + kTabOff + 16 * l) = make_uint4(e[0], e[1], e[2], e[3]);
+                *(uint2*)(lds + kStepOff + 8 * l) =
+                    make_uint2(e8[0] | (e8[1] << 8) | (e8[2] << 16) | (e8[3] << 24),
+                               e8[4] | (e8[5] << 8) | (e8[6] << 16) | (e8[7] << 24));
+                *(uint4*)(lds + kJumpOff + 16 * l) = make_uint4(jv[0] | (jv[1] << 16), jv[2] | (jv[3] << 16),
+                                                                jv[4] | (jv[5] << 16), jv[6] | (jv[7] << 16));
+                // two doublings in place (a wave's LDS reads all issue before its
+                // writes): 2, then 4 steps, stopping at a rare node or the exit
+#pragma unroll
+                for (int round = 0; round < 2; round++) {
+                    uint32_t nx[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+                        nx[i] = jump[(jv[i] & kJStop) ? 0u : (jv[i] & 1023u)];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const uint32_t s2 = ((jv[i] >> 10) & 7u) + ((nx[i] >> 10) & 7u);
+                        jv[i] = (jv[i] & kJStop) ? jv[i] : ((nx[i] & (1023u | kJStop)) | (s2 << 10));
+                    }
+                    *(uint4*)(lds + kJumpOff + 16 * l) = make_uint4(jv[0] | (jv[1] << 16), jv[2] | (jv[3] << 16),
+                                                                    jv[4] | (jv[5] << 16), jv[6] | (jv[7] << 16));
+                }
             }
             STAMP(0);
             COUNT(8, 1);
-            // ---- 2. walk: lane k keeps the k-th node (one exit, one ballot a step)
+            // ---- 2. walk: up to 4 instructions a jump; lane k keeps the k-th node
+            // when a jump starts there (one exit, one ballot a step)
             uint32_t cv = ((p - P) << 1) | (st == ST_A ? 0u : 1u);
-            uint32_t nv = 0, ev = 0, mine = 0;
+            uint32_t nv = 0, jw = 0, mine = 0, hd = 0;
             uint64_t go;
             do {
-                ev = tab16[cv];
-                const bool t = ev != 0;
-                mine = (l == nv && t) ? cv : mine;
-                nv += t ? 1u : 0u;
-                cv = t ? (ev & 0x3FFu) : cv;
-                go = __ballot(t && !(ev & 0x8000u) && nv < kWave);
+                jw = jump[cv];
+                const uint32_t s = (jw >> 10) & 7u;
+                const bool me = l == nv;
+                mine = me ? cv : mine;
+                hd = me ? s : hd;
+                nv += s;
+                cv = jw & 1023u;
+                go = __ballot(!(jw & kJStop) && nv <= kWave - 4);
             } while (go);
             const uint32_t nwalk = uni(nv);
             n = nwalk;
             cur = uni(cv);
-            rare = uni(ev) == 0;
+            rare = (uni(jw) & kJStop) && (cur >> 1) < kPiece;
+            {
+                // the nodes between jump starts: one step from the lane before, three rounds
+                uint32_t res = (l < n && hd != 0) ? 1u : 0u;
+#pragma unroll
+                for (int i = 0; i < 3; i++) {
+                    const uint32_t pm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0x138, 0xF, 0xF, true);
+                    const uint32_t pr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)res, 0x138, 0xF, 0xF, true);
+                    const bool take = l < n && !res && pr;
+                    const uint32_t e = lds[kStepOff + (pm & 511u)];
+                    const uint32_t nn = ((((pm & 511u) >> 1) + (e & 63u)) << 1) | (e >> 6);
+                    mine = take ? nn : mine;
+                    res = take ? 1u : res;
+                }
+            }
             STAMP(1);
             COUNT(9, nwalk);
 
@@ -513,8 +583,8 @@ __global__ __launch_bounds__(kWave, 4) void lzo1x_decode_seg_kernel(
                                  : (s == ST_B ? 0x801u : 1u) + (t >> 2) + (b1 << 2);
                 const uint32_t lit = !act ? 0u : run ? (t ? t + 3u : 18u + b1) : T;
                 const uint32_t lrel = r + (run ? (t ? 1u : 2u) : ilen);   // literal start, piece-relative
-                uint32_t tot = L + lit;
-                uint32_t incl = wave_incl_scan(tot);
+                const uint32_t tot = L + lit;
+                const uint32_t incl = wave_incl_scan(tot);
                 const uint32_t ok0 = op + incl - tot;            // this instruction's output position
                 const bool far = L != 0 && d > kFarT;
                 uint32_t span = lane_read(incl, n - 1);
@@ -554,17 +624,28 @@ __global__ __launch_bounds__(kWave, 4) void lzo1x_decode_seg_kernel(
                     st = stn;
                     continue;
                 }
+                // the next piece's words, unless a rare instruction comes first
+                if (!rare) {
+                    const uint32_t nP = (P + (cur >> 1)) & ~3u;
+                    if (l < kStage / 8) {
+                        const uint32_t a0 = (S.sh + nP + 8 * l) & ~3u;
+                        pf0 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0, 0, 0);
+                        pf1 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0 + 4, 0, 0);
+                        pf2 = __builtin_amdgcn_raw_buffer_load_b32(S.rs, a0 + 8, 0, 0);
+                    }
+                    pfP = nP;
+                }
                 const uint32_t O0 = op, O1 = op + span;
                 const bool farl = act2 && far;
                 const uint64_t fm = __ballot(farl);
                 flush_to(lds, O, O0 & ~(kChunk - 1));
                 STAMP(2);
-                // ---- 4. far copies: a byte a lane, one load round trip per 8 passes
+                // ---- 4. far copies: 4 bytes a lane, one load round trip per 1 KiB
                 if (fm) {
                     // Sources are more than kFarT back: below O1 - kFarT <= O0 - kChunk
                     // < O.stored, so in HBM; the ring slots of [O0, O1) hold output
                     // older than O1 - kRing < O.stored, which no near source of this
-                    // window reads (>= O0 - kFarT).
+                    // window reads (>= O0 - kFarT - kGroup).
                     __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): the stores landed
                     uint64_t rest = fm;
                     uint32_t k = (uint32_t)__builtin_ctzll(rest);
@@ -572,18 +653,22 @@ __global__ __launch_bounds__(kWave, 4) void lzo1x_decode_seg_kernel(
                     bool more = true;
                     while (more) {
                         COUNT(12, 1);
-                        uint32_t v[8], at[8];
+                        // four passes of 256 bytes, 4 a lane, one round trip
+                        uint32_t w0[4], w1[4], at[4], cnt[4], sh[4];
 #pragma unroll
-                        for (int i = 0; i < 8; i++) {
-                            at[i] = trash;
-                            v[i] = 0;
+                        for (int i = 0; i < 4; i++) {
+                            cnt[i] = 0;
+                            at[i] = sh[i] = w0[i] = w1[i] = 0;
                             if (more) {
-                                const uint32_t q = fo + c + l;
-                                const bool in = c + l < fl;
-                                at[i] = in ? (q & kRingMask) : trash;
-                                const uint32_t sp = in ? q - fd : 0u;
-                                v[i] = out_dword(O, sp) >> (8 * (sp & 3u));
-                                c += kWave;
+                                const uint32_t o = c + 4 * l;
+                                const uint32_t left = o < fl ? fl - o : 0u;
+                                cnt[i] = left < 4 ? left : 4u;
+                                at[i] = fo + o;
+                                const uint32_t sp = cnt[i] ? fo + o - fd : 0u;
+                                sh[i] = sp & 3u;
+                                w0[i] = out_dword(O, sp);
+                                w1[i] = out_dword(O, sp + 4);
+                                c += 4 * kWave;
                                 if (c >= fl) {
                                     rest &= rest - 1;
                                     more = rest != 0;
@@ -598,72 +683,154 @@ __global__ __launch_bounds__(kWave, 4) void lzo1x_decode_seg_kernel(
                             }
                         }
 #pragma unroll
-                        for (int i = 0; i < 8; i++)
-                            lds[at[i]] = (uint8_t)v[i];
+                        for (int i = 0; i < 4; i++) {
+                            const uint32_t wv = __builtin_amdgcn_alignbyte(w1[i], w0[i], sh[i]);
+#pragma unroll
+                            for (uint32_t x = 0; x < 4; x++)
+                                lds[x < cnt[i] ? ((at[i] + x) & kRingMask) : trash] = (uint8_t)(wv >> (8 * x));
+                        }
                     }
                 }
                 STAMP(3);
-                // ---- 5. rows ---------------------------------------------------------
-                // descriptors (the table is free now): code 2k+1 = match of lane k,
-                // 2k+2 = its literals, at kTabOff + 8 * (code - 1)
+                // ---- 5. rows, four at a time ----------------------------------------
+                // descriptors (the jump table is free now): code 2k+1 = match of
+                // lane k, 2k+2 = its literals, at kJumpOff + 8 * code
                 {
-                    const bool per = L > d;
-                    const uint32_t M = (per && d < kWave) ? (uint32_t)(8192.0f * __builtin_amdgcn_rcpf((float)d)) + 1u : 0u;
-                    const uint32_t hm = d | (M << 16) | (per ? kPer : 0u) | (far ? kFar : 0u);
-                    const uint32_t lb = kStageOff + lrel - (ok0 + L);
-                    *(uint4*)(lds + kTabOff + 16 * l) = make_uint4(ok0, hm, lb, 0u);
+                    const bool pers = L > d && d < 256;
+                    const uint32_t M = pers ? (uint32_t)(65536.0f * __builtin_amdgcn_rcpf((float)d)) + 1u : 0u;
+                    const uint32_t hm = far ? (d | kFar) : pers ? (d | (M << 8) | kPerS) : d;
+                    *(uint2*)(lds + kJumpOff + 16 * l + 8) = make_uint2(ok0, hm);
+                    *(uint2*)(lds + kJumpOff + 16 * l + 16) = make_uint2(kStageOff + lrel - (ok0 + L), 0u);
+                    if (l == 0)                          // code 0: bytes before the window's first segment
+                        *(uint2*)(lds + kJumpOff) = make_uint2(0u, kFar);
                 }
                 const uint32_t e1 = (act2 && L) ? ok0 : 0xFFFFFFFFu;
                 const uint32_t e2 = (act2 && lit) ? ok0 + L : 0xFFFFFFFFu;
                 uint32_t carry = 0;
-                for (uint32_t R = O0 & ~(kWave - 1); R < O1; R += kWave) {
-                    if (R + kWave - O.stored > kRing)
-                        flush_to(lds, O, R & ~(kChunk - 1));
-                    const uint32_t a1 = e1 - R, a2 = e2 - R;
-                    const bool s1 = a1 < kWave, s2 = a2 < kWave;
-                    uint32_t g = carry;
+#ifdef POM_SEG_NOROWS
+                for (uint32_t R = O1; R < O1; R += kGroup) {   // (timing counterfactual: no rows)
+#else
+                for (uint32_t R = O0 & ~(kWave - 1); R < O1; R += kGroup) {
+#endif
                     COUNT(10, 1);
-                    if (__ballot(s1 || s2)) {
+                    if (R + kGroup - O.stored > kRing)
+                        flush_to(lds, O, R & ~(kChunk - 1));
+                    // segment codes: a running maximum over the group's marked starts
+                    const uint32_t a1 = e1 - R, a2 = e2 - R;
+                    uint32_t m[kRows];
+#pragma unroll
+                    for (int j = 0; j < kRows; j++)
+                        m[j] = 0;
+                    if (__ballot(a1 < kGroup || a2 < kGroup)) {
                         COUNT(14, 1);
-                        lds[kMarkOff + l] = 0;
-                        lds[s1 ? kMarkOff + a1 : trash] = (uint8_t)(2 * l + 1);
-                        lds[s2 ? kMarkOff + a2 : trash] = (uint8_t)(2 * l + 2);
-                        g = umax(wave_incl_max(lds[kMarkOff + l]), carry);
+                        if (kRows == 4)
+                            *(uint32_t*)(lds + kMarkOff + 4 * l) = 0;
+                        else if (kRows == 2)
+                            *(uint16_t*)(lds + kMarkOff + 2 * l) = 0;
+                        else
+                            lds[kMarkOff + l] = 0;
+                        lds[a1 < kGroup ? kMarkOff + a1 : trash] = (uint8_t)(2 * l + 1);
+                        lds[a2 < kGroup ? kMarkOff + a2 : trash] = (uint8_t)(2 * l + 2);
+#pragma unroll
+                        for (int j = 0; j < kRows; j++)
+                            m[j] = lds[kMarkOff + kWave * j + l];
+#pragma unroll
+                        for (int j = 0; j < kRows; j++)
+                            m[j] = wave_incl_max(m[j]);
                     }
-                    const uint32_t pp = R + l;
-                    const bool valid = g != 0 && pp < O1;
-                    const uint2 dsc = *(const uint2*)(lds + kTabOff + 8 * (g ? g - 1 : 0u));
-                    const bool islit = (g & 1u) == 0;
-                    const uint32_t hi = islit ? 0u : dsc.y;
-                    const uint32_t dd = hi & 0xFFFFu, Mg = (hi >> 16) & 0x3FFFu;
-                    // match: the byte d back, or for a periodic match the congruent
-                    // byte of the period before max(row, segment start)
-                    const uint32_t xb = g == carry ? R : dsc.x;
-                    const uint32_t x = pp - xb;
-                    const uint32_t rm = (hi & kPer) && dd < kWave ? x - dd * ((x * Mg) >> 13) : x;
-                    const uint32_t sp = xb - dd + rm;
-                    const bool act3 = valid && !(hi & kFar);
-                    const bool ready = islit || sp < R;
-                    const uint32_t addr = islit ? dsc.x + pp : (sp & kRingMask);
-                    const bool wr = act3 && ready;
-                    const uint8_t v = lds[wr ? addr : trash];
-                    lds[wr ? (pp & kRingMask) : trash] = v;
-                    uint64_t pend = __ballot(act3 && !ready);
-                    if (pend) {
-                        // sources inside the row: each sub-pass moves the bytes whose
-                        // source byte is final
-                        bool pl = act3 && !ready;
-                        const uint32_t j = sp - R;
-                        while (pend) {
+                    uint32_t g[kRows], c[kRows + 1];
+                    c[0] = carry;
+#pragma unroll
+                    for (int j = 0; j < kRows; j++) {
+                        g[j] = umax(m[j], c[j]);
+                        c[j + 1] = umax(c[j], uni(lane_read(m[j], kWave - 1)));
+                    }
+                    carry = c[kRows];
+                    uint2 dsc[kRows];
+#pragma unroll
+                    for (int j = 0; j < kRows; j++)
+                        dsc[j] = *(const uint2*)(lds + kJumpOff + 8 * g[j]);
+                    // sources: a staged literal, or the ring byte d back -- for a
+                    // period d, the congruent byte of the period before the group
+                    // or the segment start (x = pp - xb < kGroup)
+                    uint32_t addr[kRows], wr[kRows], sp[kRows];
+                    bool pd[kRows];
+#pragma unroll
+                    for (int j = 0; j < kRows; j++) {
+                        const uint32_t pp = R + kWave * j + l;
+                        const bool islit = (g[j] & 1u) == 0;
+                        const uint32_t hi = dsc[j].y;
+                        const bool ps = (hi & kPerS) != 0;
+                        const uint32_t dd = hi & (ps ? 0xFFu : 0xFFFFu);
+                        const uint32_t Mg = (hi >> 8) & 0x1FFFFu;
+                        // (a segment that started before the group: R; a literal's
+                        // xb does not matter)
+                        const uint32_t xb = umax(R, dsc[j].x);
+                        const uint32_t x = pp - xb;
+                        const uint32_t rm = ps ? x - __umul24(dd, __umul24(x, Mg) >> 16) : x;
+                        sp[j] = xb - dd + rm;
+                        const bool act3 = pp < O1 && !(hi & kFar);   // (code 0 is kFar)
+                        const bool rdy = islit || sp[j] < R;
+                        addr[j] = islit ? dsc[j].x + pp : (sp[j] & kRingMask);
+                        wr[j] = (act3 && rdy) ? (pp & kRingMask) : trash;
+                        addr[j] = (act3 && rdy) ? addr[j] : trash;
+                        pd[j] = act3 && !rdy;
+                    }
+                    uint8_t v[kRows];
+#pragma unroll
+                    for (int j = 0; j < kRows; j++)
+                        v[j] = lds[addr[j]];
+#pragma unroll
+                    for (int j = 0; j < kRows; j++)
+                        lds[wr[j]] = v[j];
+                    uint64_t pm[kRows];
+                    uint64_t pany = 0;
+#pragma unroll
+                    for (int j = 0; j < kRows; j++)
+                        pany |= (pm[j] = __ballot(pd[j]));
+#ifdef POM_SEG_NOSUB
+                    pany = 0;                            // (timing counterfactual: output not exact)
+#endif
+                    if (pany) {
+                        // sources inside the group: each sub-pass moves the bytes
+                        // whose source byte is final
+                        for (;;) {
                             COUNT(11, 1);
-                            const bool go2 = pl && ((~pend >> j) & 1ull);
-                            const uint8_t v2 = lds[go2 ? addr : trash];
-                            lds[go2 ? (pp & kRingMask) : trash] = v2;
-                            pl = pl && !go2;
-                            pend = __ballot(pl);
+                            uint32_t ad2[kRows], wr2[kRows];
+                            bool go2[kRows];
+#pragma unroll
+                            for (int j = 0; j < kRows; j++) {
+                                if (!pm[j]) {
+                                    go2[j] = false;
+                                    ad2[j] = wr2[j] = trash;
+                                    continue;
+                                }
+                                const uint32_t o = sp[j] - R;
+                                uint64_t sel = pm[0];
+#pragma unroll
+                                for (int jj = 1; jj < kRows; jj++)
+                                    sel = o >= kWave * jj ? pm[jj] : sel;
+                                go2[j] = pd[j] && !((sel >> (o & 63u)) & 1ull);
+                                ad2[j] = go2[j] ? (sp[j] & kRingMask) : trash;
+                                wr2[j] = go2[j] ? ((R + kWave * j + l) & kRingMask) : trash;
+                            }
+                            uint8_t v2[kRows];
+#pragma unroll
+                            for (int j = 0; j < kRows; j++)
+                                v2[j] = lds[ad2[j]];
+#pragma unroll
+                            for (int j = 0; j < kRows; j++)
+                                lds[wr2[j]] = v2[j];
+                            pany = 0;
+#pragma unroll
+                            for (int j = 0; j < kRows; j++) {
+                                pd[j] = pd[j] && !go2[j];
+                                pany |= (pm[j] = __ballot(pd[j]));
+                            }
+                            if (!pany)
+                                break;
                         }
                     }
-                    carry = uni(lane_read(g, kWave - 1));
                 }
                 op = O1;
                 p = P + (cur >> 1);

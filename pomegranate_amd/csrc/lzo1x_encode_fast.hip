@@ -1027,17 +1027,12 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
 
 }  // namespace
 
-// Waves per block of the global-dictionary encoder: POM_ENC_WAVES (1 or 2,
-// read at every launch, for A/B runs and the tests of both kernels), default
-// POM_ENC_WAVES_DEFAULT.
-#ifndef POM_ENC_WAVES_DEFAULT
-#define POM_ENC_WAVES_DEFAULT 1
-#endif
+// Waves per block of the global-dictionary encoder: debug key enc_waves of
+// POM_LZO_DEBUG (1 or 2, read at every launch, for the tests of both
+// kernels), default 1.
 static int enc_waves(void)
 {
-    const char* e = getenv("POM_ENC_WAVES");
-    const int w = e ? atoi(e) : POM_ENC_WAVES_DEFAULT;
-    return w == 1 ? 1 : 2;
+    return pom_dbg_int("enc_waves", 1) == 2 ? 2 : 1;
 }
 
 static uint32_t enc_resident(void)
@@ -1057,14 +1052,13 @@ static uint32_t enc_resident(void)
 
 // Grid of the global-dictionary encoders: one workgroup per dictionary region
 // of the scratch, at most one per block and one per resident slot, and at
-// most POM_ENC_GRID (tests: a grid smaller than the batch).
+// most the debug key enc_grid.
 static uint32_t enc_grid(size_t scratch_bytes, uint32_t nblocks)
 {
     uint32_t grid = scratch_bytes > kScratchHead ? (uint32_t)((scratch_bytes - kScratchHead) / kDictBytes) : 0u;
     grid = grid < nblocks ? grid : nblocks;
     grid = grid < enc_resident() ? grid : enc_resident();
-    const char* e = getenv("POM_ENC_GRID");
-    const uint32_t cap = e ? (uint32_t)atoi(e) : 0u;
+    const uint32_t cap = (uint32_t)pom_dbg_int("enc_grid", 0);   // (tests: a grid smaller than the batch)
     return cap && cap < grid ? cap : grid;
 }
 

@@ -27,6 +27,43 @@
 #include "lzo_mi355x_kernels.h"
 #include "minilzo.h"
 
+/* Debug and experiment switches: ONE environment variable, POM_LZO_DEBUG,
+ * a comma-separated list of key=value.  No product path
+ * needs it; an unset key takes its default.  Keys: decoder=fast|seg|win
+ * (device batches), sc_copy=1, sc_combine=0, sc_lat=0, sc_lat_min=BYTES,
+ * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, enc_lds_max=N, enc_waves=1|2,
+ * enc_grid=N.  Read at every use (tests change it between calls). */
+const char *pom_dbg_str(const char *key, char *buf, size_t n)
+{
+    const char *e = getenv("POM_LZO_DEBUG");
+    const size_t kl = strlen(key);
+    if (!e || !n)
+        return NULL;
+    for (const char *p = e; *p;) {
+        const char *end = strchr(p, ',');
+        const size_t len = end ? (size_t)(end - p) : strlen(p);
+        if (len > kl && strncmp(p, key, kl) == 0 && p[kl] == '=') {
+            size_t vl = len - kl - 1;
+            if (vl >= n)
+                vl = n - 1;
+            memcpy(buf, p + kl + 1, vl);
+            buf[vl] = 0;
+            return buf;
+        }
+        if (!end)
+            break;
+        p = end + 1;
+    }
+    return NULL;
+}
+
+long pom_dbg_int(const char *key, long dflt)
+{
+    char buf[32];
+    const char *v = pom_dbg_str(key, buf, sizeof buf);
+    return v && *v ? atol(v) : dflt;
+}
+
 #define ALIGN_UP(x, a) (((x) + (size_t)(a) - 1) & ~((size_t)(a) - 1))
 
 /* ------------------------------------------------------------------------ */
@@ -252,18 +289,15 @@ size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
 /* Which throughput decoder a batch uses: the op-set decoder
  * (lzo1x_decode_fast.hip: 16 blocks per CU) or the windowed one
  * (lzo1x_decode_win.hip: 2 blocks per CU, a 64 KiB LDS output ring, never
- * reads its own output back).  POM_DECODER=fast|win|ser|row forces one (ser,
- * row: lzo1x_decode_ser.hip); single calls
- * always use the windowed one (see single_call). */
+ * reads its own output back).  Debug key decoder=fast|win|seg forces one;
+ * single calls always use the windowed one (see single_call). */
+enum { DEC_FAST = 0, DEC_WIN = 1, DEC_SEG = 2 };
 static int use_win_decoder(uint32_t nblocks)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("POM_DECODER");
-        v = !e ? 3 : strcmp(e, "win") == 0 ? 1 : strcmp(e, "ser") == 0 ? 2 : strcmp(e, "row") == 0 ? 4 : 0;
-    }
-    if (v != 3)
-        return v;
+    char buf[16];
+    const char *e = pom_dbg_str("decoder", buf, sizeof buf);
+    if (e)
+        return strcmp(e, "win") == 0 ? DEC_WIN : strcmp(e, "seg") == 0 ? DEC_SEG : DEC_FAST;
     /* default: the windowed decoder while the batch fits two workgroups per
      * CU (one round; lone blocks decode 1.3-1.5x faster there), the op-set
      * decoder for larger batches (16 blocks per CU) */
@@ -273,16 +307,11 @@ static int use_win_decoder(uint32_t nblocks)
 
 /* Single calls: the kernels write the output and its length/status straight
  * into the pinned host staging (mapped, coherent: hipHostMalloc's default), so
- * nothing is copied back but what was produced.  POM_SC_COPY=1: the round-2
+ * nothing is copied back but what was produced.  debug key sc_copy=1: the round-2
  * path (device staging, one D2H copy of the whole room). */
 static int sc_zero_copy(void)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("POM_SC_COPY");
-        v = !(e && strcmp(e, "1") == 0);
-    }
-    return v;
+    return pom_dbg_int("sc_copy", 0) != 1;
 }
 
 /* Throughput decoder over the whole batch, then the exact decoder over the blocks
@@ -319,14 +348,13 @@ static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, cons
     const uint32_t nsets = (uint32_t)scr_sets(nblocks);
     uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nblocks));
     if (win) {
-        /* the windowed (win == 1), table-walk (win == 2) or row (win == 4)
-         * decoder: no op sets, only the fallback list */
+        /* the windowed (DEC_WIN) or segment-row (DEC_SEG) decoder: no op sets,
+         * only the fallback list */
         if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
             return -1;
-        if ((win == 2   ? lzo_mi355x_launch_decompress_ser
-             : win == 4 ? lzo_mi355x_launch_decompress_row
-                        : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
-                                                            out_len, status, fb, ids, nblocks, s) != 0)
+        if ((win == DEC_SEG ? lzo_mi355x_launch_decompress_seg
+                            : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
+                                                                out_len, status, fb, ids, nblocks, s) != 0)
             return -1;
     } else {
         if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)
@@ -558,7 +586,7 @@ struct hbatch {
     int nslots;             /* chunks in flight per device (<= kSlots) */
 };
 
-/* POM_HOST_TIMING=1: per-batch and per-chunk wall times on stderr (diagnostic) */
+/* debug key host_timing=1: per-batch and per-chunk wall times on stderr (diagnostic) */
 static int g_timing = -1;
 
 static double now_ms(void)
@@ -574,7 +602,7 @@ static const size_t kLatMaxScratch = (size_t)1 << 30;
 static int use_lat_decoder(size_t z);
 static int lat_reserve(struct slot *t, size_t bytes);
 
-/* A decompress chunk of at most 8 blocks, each of at least POM_SC_LAT_MIN
+/* A decompress chunk of at most 8 blocks, each of at least sc_lat_min (debug key, default 2048)
  * compressed bytes, decodes on one latency-decoder pipeline (the whole GPU on
  * these few blocks; lzo1x_decode_lat.hip) with the exact decoder behind it for
  * the blocks it hands over.  1 launched, 0 not eligible (nothing launched),
@@ -739,7 +767,7 @@ static int chunk_deliver(struct slot *S, struct layout *L, const struct hbatch *
  * copies, the kernels of several chunks and the host-side packing overlap.
  * The first chunk, the largest blocks, gets a quarter of the budget: their
  * long serial LZ chains start while the rest of the batch is still being
- * copied up.  POM_LZO_CHUNK_MB overrides the budget. */
+ * copied up.  Debug key chunk_mb overrides the budget. */
 static const size_t kChunkBudget = (size_t)128 << 20;
 static const size_t kChunkBlocks = (size_t)1 << 20;
 /* below this many bytes per device a batch stays on one device */
@@ -830,10 +858,8 @@ static int batch_devices(int *devs)
 static int batch_common(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
                         uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks)
 {
-    if (g_timing < 0) {
-        const char *e = getenv("POM_HOST_TIMING");
-        g_timing = e && *e == '1';
-    }
+    if (g_timing < 0)
+        g_timing = pom_dbg_int("host_timing", 0) == 1;
     const double t0 = g_timing ? now_ms() : 0;
     struct tctx *t = tctx_get();
     if (!t)
@@ -869,16 +895,13 @@ static int batch_common(enum op_kind kind, const uint8_t *const *src, const size
     /* compress chunks that fit the LDS encoder's 4 blocks per CU at once use
      * it: a block alone on its CU finishes twice as fast as with the
      * dictionaries in HBM (that encoder wins only on full GPUs: 16 per CU) */
-    B.enc_lds_max = lzo_mi355x_fast_resident_blocks() / 4;
-    const char *el = getenv("POM_ENC_LDS_MAX");
-    if (el)
-        B.enc_lds_max = (uint32_t)atol(el);
-    const char *ns = getenv("POM_LZO_SLOTS");
-    if (ns && atoi(ns) >= 1 && atoi(ns) <= kSlots)
-        B.nslots = atoi(ns);
-    const char *e = getenv("POM_LZO_CHUNK_MB");
-    if (e && atol(e) > 0)
-        B.budget = (size_t)atol(e) << 20;
+    B.enc_lds_max = (uint32_t)pom_dbg_int("enc_lds_max", (long)(lzo_mi355x_fast_resident_blocks() / 4));
+    const long ns = pom_dbg_int("slots", kSlots);
+    if (ns >= 1 && ns <= kSlots)
+        B.nslots = (int)ns;
+    const long mb = pom_dbg_int("chunk_mb", 0);
+    if (mb > 0)
+        B.budget = (size_t)mb << 20;
     int rc = LZO_E_OUT_OF_MEMORY;
     if (pom_plan_make(&B.plan, nblocks, cost, ndev, kSplitMinBytes) == 0) {
         /* blocks a failed device leaves untouched read as errors */
@@ -954,7 +977,7 @@ const char *lzo_version_date(void) { return LZO_VERSION_DATE; }
  * mds/itb.c:2964) are COMBINED: the first caller becomes the leader and runs
  * every call queued behind it (of the same kind, up to kScGroup) as one
  * launch on its own stream; the others sleep until their result is in their
- * buffer.  A lone call is a group of one.  POM_SC_COMBINE=0 turns combining
+ * buffer.  A lone call is a group of one.  Debug key sc_combine=0 turns combining
  * off (every call its own launch, as in round 2).
  * Staging of a group of k calls (device and pinned host alike):
  *   [0, H)          header arrays: src_off u64[k], dst_off u64[k], src_len[k],
@@ -1007,12 +1030,7 @@ static void sc_init(void)
 
 static int sc_combine(void)
 {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("POM_SC_COMBINE");
-        v = !(e && strcmp(e, "0") == 0);
-    }
-    return v;
+    return pom_dbg_int("sc_combine", 1) != 0;
 }
 
 /* header arrays of a group of k */
@@ -1068,17 +1086,12 @@ static struct slot *sc_slot(struct sc_queue *q)
  * 32 KiB up to 536 KB, where the windowed decoder's one workgroup takes
  * 0.14-2.2 ms); shorter ones (equal at 12 KB) the windowed decoder, and so
  * does a combined group with any such call or more than 8 calls (see
- * lat_group).  POM_SC_LAT_MIN sets the threshold (bytes of compressed input),
- * POM_SC_LAT=0 turns it off. */
+ * lat_group).  Debug keys: sc_lat_min sets the threshold (bytes of compressed
+ * input), sc_lat=0 turns it off. */
 static int use_lat_decoder(size_t z)
 {
-    static long min_z = -1;
-    if (min_z < 0) {
-        const char *off = getenv("POM_SC_LAT");
-        const char *e = getenv("POM_SC_LAT_MIN");
-        min_z = off && strcmp(off, "0") == 0 ? 0x7FFFFFFFL : e && atol(e) > 0 ? atol(e) : 2048L;
-    }
-    return z >= (size_t)min_z;
+    const long min_z = pom_dbg_int("sc_lat", 1) == 0 ? 0x7FFFFFFFL : pom_dbg_int("sc_lat_min", 2048L);
+    return z >= (size_t)(min_z > 0 ? min_z : 2048L);
 }
 
 
@@ -1103,7 +1116,7 @@ static int lat_reserve(struct slot *t, size_t bytes)
     return 0;
 }
 
-/* A group of k <= 8 decodes of at least POM_SC_LAT_MIN compressed bytes each
+/* A group of k <= 8 decodes of at least sc_lat_min compressed bytes each
  * runs as ONE latency-decoder pipeline (lzo1x_decode_lat.hip: the blocks side
  * by side in every kernel).  Returns 1 when launched, 0 when the group does
  * not qualify (nothing launched), -1 on a launch error.  (Separate pipelines
@@ -1137,9 +1150,7 @@ static int lat_group(struct slot *t, struct sc_req **g, int k, const uint8_t *d,
 static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
 {
     const enum sc_kind kind = g[0]->kind;
-    static int trace = -1;
-    if (trace < 0)
-        trace = getenv("POM_SC_TRACE") != NULL;
+    const int trace = pom_dbg_int("sc_trace", 0) == 1;
     const double t0 = trace ? now_ms() : 0.0;
     for (int i = 0; i < k; i++)
         g[i]->rc = LZO_E_ERROR;

@@ -81,17 +81,9 @@ int lzo_mi355x_launch_decompress_win(const uint8_t *src, const uint64_t *src_off
                                      uint32_t *out_len, int32_t *status, uint32_t *fallback,
                                      uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
 
-/* Table-walk throughput decoder (lzo1x_decode_ser.hip): one wave per block,
- * an 8 KiB LDS output ring, 16-17 blocks per CU.  Fallback list as above. */
-int lzo_mi355x_launch_decompress_ser(const uint8_t *src, const uint64_t *src_off,
-                                     const uint32_t *src_len, uint8_t *dst,
-                                     const uint64_t *dst_off, const uint32_t *dst_cap,
-                                     uint32_t *out_len, int32_t *status, uint32_t *fallback,
-                                     uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
-
-/* The table-walk walker with the row executor (lzo1x_decode_ser.hip, ROWS):
- * output rows of 256 bytes resolved to final origins.  Same arguments. */
-int lzo_mi355x_launch_decompress_row(const uint8_t *src, const uint64_t *src_off,
+/* Segment-row throughput decoder (lzo1x_decode_seg.hip): one wave per block,
+ * an 8 KiB LDS output ring, 16 blocks per CU.  Fallback list as above. */
+int lzo_mi355x_launch_decompress_seg(const uint8_t *src, const uint64_t *src_off,
                                      const uint32_t *src_len, uint8_t *dst,
                                      const uint64_t *dst_off, const uint32_t *dst_cap,
                                      uint32_t *out_len, int32_t *status, uint32_t *fallback,
@@ -128,6 +120,11 @@ int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off
                                      const uint32_t *src_len, uint32_t *out_len,
                                      int32_t *status, uint32_t nblocks, uint32_t *cap_out,
                                      uint32_t cap_limit, hipStream_t stream);
+
+/* Host side (lzo_host.c), not part of the ABI: the debug switches of
+ * POM_LZO_DEBUG ("key=value,..."; NULL / dflt when the key is absent). */
+const char *pom_dbg_str(const char *key, char *buf, size_t n);
+long pom_dbg_int(const char *key, long dflt);
 
 /* Host side (lzo_host.c), not part of the ABI: len[i] bytes from src[i] to
  * dst[i] for every i, split over up to 8 threads once the total is large. */

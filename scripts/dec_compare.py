@@ -25,10 +25,12 @@ fast.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctyp
 win = lib.lzo_mi355x_launch_decompress_win
 win.restype = ctypes.c_int
 win.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
-ser = lib.lzo_mi355x_launch_decompress_ser
+# the table-walk and row decoders are experiments outside the product library
+_exp = ctypes.CDLL(os.path.join(ROOT, "scripts", "experiments", "libdecode_ser.so"))
+ser = _exp.lzo_mi355x_launch_decompress_ser
 ser.restype = ctypes.c_int
 ser.argtypes = win.argtypes
-row = lib.lzo_mi355x_launch_decompress_row
+row = _exp.lzo_mi355x_launch_decompress_row
 row.restype = ctypes.c_int
 row.argtypes = win.argtypes
 lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t

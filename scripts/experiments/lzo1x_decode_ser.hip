@@ -39,7 +39,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#include "lzo_mi355x_kernels.h"
+#include "lzo_mi355x_kernels.h"   // (built by scripts/experiments/Makefile, outside the product library)
 
 namespace {
 

@@ -54,7 +54,18 @@ def setup(sizes, seed):
     return src, zb, zl, nb
 
 
+def variant(kind):
+    """kind "seg@path.so": the seg launcher of a variant build (scripts/ab/)."""
+    if "@" in kind and kind not in one:
+        v = ctypes.CDLL(os.path.join(ROOT, kind.split("@", 1)[1]))
+        f = v.lzo_mi355x_launch_decompress_seg
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]
+        one[kind] = f
+
+
 def run(kind, src, zb, zl, nb, reps):
+    variant(kind)
     out = torch.zeros_like(src.arena)
     ol = torch.zeros_like(zl)
     st = torch.zeros_like(zl)

@@ -577,10 +577,8 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
     """Each throughput encoder kernel (global dictionary with one or two waves
     per block, LDS dictionary) byte-identical to the oracle on the sweep's
     content models, sizes up to 300 KB, more blocks than one grid holds."""
-    if kernel == "gdict_two_wave":
-        monkeypatch.setenv("POM_ENC_WAVES", "2")
-    elif kernel == "gdict_one_wave":
-        monkeypatch.setenv("POM_ENC_WAVES", "1")
+    waves = "enc_waves=2" if kernel == "gdict_two_wave" else "enc_waves=1"
+    monkeypatch.setenv("POM_LZO_DEBUG", waves)          # (lzo_host.c pom_dbg_str)
     blocks = _sweep_blocks(300, 91)
     src = gu.device_batch(torch, blocks, dev, shift=1)
     dst = gu.empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
@@ -592,7 +590,7 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
         # a grid of 40 workgroups: each dictionary region serves several blocks,
         # taken through the block ticket (scratch sized for the batch, as the
         # ABI requires; its ticket word starts as garbage)
-        monkeypatch.setenv("POM_ENC_GRID", "40")
+        monkeypatch.setenv("POM_LZO_DEBUG", waves + ",enc_grid=40")
         scr = torch.full((lzo.compress_scratch_bytes(len(blocks)),), 0x5A, dtype=torch.uint8, device=dev)
         lzo.compress_dev(src, dst, olen, st, scratch=scr)
     torch.cuda.synchronize()
@@ -642,7 +640,7 @@ def test_encoder_block_tickets_mixed_sizes(dev, gu):
     assert torch.equal(back, src.arena)
 
 
-@pytest.mark.parametrize("kind", ["win", "ser", "row", "seg"])
+@pytest.mark.parametrize("kind", ["win", "seg"])
 def test_window_decoder_every_valid_stream(dev, gu, kind):
     """The windowed (lzo1x_decode_win.hip) and table-walk
     (lzo1x_decode_ser.hip) decoders alone, without the exact decoder behind it: every content model (incompressible blocks with
@@ -668,7 +666,7 @@ def test_window_decoder_every_valid_stream(dev, gu, kind):
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("kind", ["win", "ser", "row", "seg"])
+@pytest.mark.parametrize("kind", ["win", "seg"])
 def test_window_decoder_full_grammar_streams(dev, gu, kind):
     """LZO1X streams the LZO1X-1 compressor never writes (M1 after literal runs
     and trailing literals, long extensions, first runs of 1-3 bytes) decode
@@ -684,7 +682,7 @@ def test_window_decoder_full_grammar_streams(dev, gu, kind):
     assert outs == want
 
 
-@pytest.mark.parametrize("kind", ["win", "ser", "row", "seg"])
+@pytest.mark.parametrize("kind", ["win", "seg"])
 def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, kind, malformed):
     """Malformed streams, and valid streams whose output does not fit, are
     handed to the exact decoder (status 0x7FFF0001 until it runs) -- never
@@ -772,6 +770,26 @@ def test_lone_single_calls_on_the_latency_decoder(dev, oracle):
         cut = z[: len(z) // 2]
         rc, _ = lzo.lzo1x_decompress_safe(cut, n)
         assert rc == oracle.decompress_safe(cut, n)[0]
+
+
+def test_latency_decoder_zero_runs_stay_linear(dev, oracle):
+    """Zero-run input through the single-call path (the latency decoder from
+    2 KB of compressed input): 2 MB of zero bytes as a stream, a valid stream
+    of 8 MiB of zeros (a length extension of ~33 K zero bytes) and one with a
+    4 MiB zero run between two ITB blocks.  Codes, lengths and bytes equal the
+    reference's; each call takes well under a second (every node of a zero
+    run used to scan the rest of the run: O(z^2))."""
+    import time
+    cases = [(bytes(2 << 20), 1 << 20)]
+    for d in (bytes(8 << 20), synth.block(synth.ITB, 71, 65536) + bytes(4 << 20) + synth.block(synth.ITB, 72, 65536)):
+        cases.append((oracle.compress(d), len(d)))
+    for z, cap in cases:
+        t0 = time.perf_counter()
+        rc, out = lzo.lzo1x_decompress_safe(z, cap)
+        dt = time.perf_counter() - t0
+        want = oracle.decompress_safe(z, cap)
+        assert (rc, out) == want
+        assert dt < 1.0, dt
 
 
 @pytest.mark.parametrize("k", [1, 3, 8])
