@@ -810,8 +810,10 @@ def run_single(args, lzo, synth):
         "value": v, "unit": "us", "n_gpus": 1, "steps": max(3, args.steps), "warmup": 1,
         "higher_is_better": False, "scaling": "none", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic ITB payload images", "config": {
-            "workload": "minilzo.h single calls (host buffers in, host buffers out: H2D, "
-                        "kernels, D2H, one stream sync per call) vs lib/minilzo.c on one core"},
+            "workload": "minilzo.h single calls (host buffers in, host buffers out: one H2D copy, "
+                        "kernels writing into mapped pinned staging, one stream sync per call; "
+                        "calls from several threads combined into shared launches) "
+                        "vs lib/minilzo.c on one core"},
         "calls": out, "concurrent": conc}
     return result, errors
 

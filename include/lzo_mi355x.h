@@ -55,8 +55,9 @@ size_t lzo_mi355x_compress_scratch(uint32_t nblocks);
  * block.  After the call, the u32 at scratch byte 0 counts the blocks the
  * throughput decoder handed to the exact (one wave per block, ~20x slower)
  * decoder: malformed streams, capacity or look-behind errors, destinations not
- * 16-byte aligned, empty or >= 16 MiB inputs.  Every valid stream with an
- * aligned destination stays on the throughput decoder. */
+ * 16-byte aligned (the windowed decoder, which small batches take, needs only
+ * 8), empty or >= 16 MiB inputs.  Every valid stream with a 16-byte aligned
+ * destination stays on the throughput decoders. */
 int lzo_mi355x_decompress_dev(const uint8_t *src, const uint64_t *src_off,
                               const uint32_t *src_len, uint8_t *dst,
                               const uint64_t *dst_off, const uint32_t *dst_cap,

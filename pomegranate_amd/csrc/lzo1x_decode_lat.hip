@@ -438,7 +438,7 @@ __device__ uint32_t block_scan(uint32_t v, uint32_t* sh)
 }
 
 template <bool MAX>
-__global__ __launch_bounds__(kScanT) void scan_tiles(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(kScanT) void scan_tiles(const uint32_t* in, uint32_t* out,   // (in == out: in-place scans)
                                                      uint32_t n, uint32_t* __restrict__ tiles)
 {
     __shared__ uint32_t sh[kScanT];

@@ -105,8 +105,6 @@ struct slot {
     size_t dcap;
     uint8_t *hmem;
     size_t hcap;
-    void *lat;                  /* single calls: the latency decoder's scratch */
-    size_t latcap;
 };
 
 /* A host thread's resources on one device: kSlots slots, so that several
@@ -143,8 +141,6 @@ static void tctx_free(void *p)
                 hipFree(c->s[k].dmem);
             if (c->s[k].hmem)
                 hipHostFree(c->s[k].hmem);
-            if (c->s[k].lat)
-                hipFree(c->s[k].lat);
             hipStreamDestroy(c->s[k].stream);
         }
     }
@@ -306,8 +302,10 @@ static int use_win_decoder(uint32_t nblocks)
 }
 
 /* Single calls: the kernels write the output and its length/status straight
- * into the pinned host staging (mapped, coherent: hipHostMalloc's default), so
- * nothing is copied back but what was produced.  debug key sc_copy=1: the round-2
+ * into the pinned host staging (hipHostMalloc, mapped into the device's
+ * address space), so nothing is copied back but what was produced; the
+ * caller reads it only after the stream synchronisation, which is what makes
+ * the kernels' writes visible to the host.  debug key sc_copy=1: the round-2
  * path (device staging, one D2H copy of the whole room). */
 static int sc_zero_copy(void)
 {
@@ -596,11 +594,73 @@ static double now_ms(void)
     return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
-/* the latency decoder's scratch at most (a group needing more, from ~4 MB of
- * compressed input, takes the windowed decoder) */
-static const size_t kLatMaxScratch = (size_t)1 << 30;
+/* The latency decoder's scratch: ONE buffer per device, shared by every
+ * thread's host-batch chunks and combined single-call groups (ADVICE round
+ * 3: per-thread, per-slot buffers of up to 1 GiB each pinned GBs of HBM).
+ * A user holds the mutex while it launches, waits (on the GPU, through the
+ * event) for the previous use's kernels, and records its own.  Groups needing
+ * more than kLatMaxScratch (from ~1 MB of compressed input) take the windowed
+ * decoder. */
+static const size_t kLatMaxScratch = (size_t)256 << 20;
+struct lat_scratch {
+    pthread_mutex_t mu;
+    void *buf;
+    size_t cap;
+    hipEvent_t done;            /* the last use's kernels (created with the buffer) */
+};
+static struct lat_scratch lat_s[kMaxDev];
+static pthread_once_t lat_once = PTHREAD_ONCE_INIT;
+
+static void lat_init(void)
+{
+    for (int d = 0; d < kMaxDev; d++)
+        pthread_mutex_init(&lat_s[d].mu, NULL);
+}
+
+/* The device's scratch, at least `bytes`, locked, with stream s ordered
+ * after its last use; NULL (unlocked) if the device or memory is missing. */
+static struct lat_scratch *lat_acquire(size_t bytes, hipStream_t s)
+{
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev || bytes > kLatMaxScratch)
+        return NULL;
+    pthread_once(&lat_once, lat_init);
+    struct lat_scratch *L = &lat_s[dev];
+    pthread_mutex_lock(&L->mu);
+    if (!L->done && hipEventCreateWithFlags(&L->done, hipEventDisableTiming) != hipSuccess) {
+        L->done = NULL;
+        pthread_mutex_unlock(&L->mu);
+        return NULL;
+    }
+    if (L->cap < bytes) {
+        hipEventSynchronize(L->done);           /* (a never-recorded event is complete) */
+        if (L->buf)
+            hipFree(L->buf);
+        L->buf = NULL;
+        L->cap = 0;
+        size_t want = ALIGN_UP(bytes + bytes / 4, (size_t)1 << 20);
+        want = want < kLatMaxScratch ? want : kLatMaxScratch;
+        if (hipMalloc(&L->buf, want) != hipSuccess) {
+            L->buf = NULL;
+            pthread_mutex_unlock(&L->mu);
+            return NULL;
+        }
+        L->cap = want;
+    }
+    if (hipStreamWaitEvent(s, L->done, 0) != hipSuccess) {
+        pthread_mutex_unlock(&L->mu);
+        return NULL;
+    }
+    return L;
+}
+
+static void lat_release(struct lat_scratch *L, hipStream_t s)
+{
+    hipEventRecord(L->done, s);
+    pthread_mutex_unlock(&L->mu);
+}
+
 static int use_lat_decoder(size_t z);
-static int lat_reserve(struct slot *t, size_t bytes);
 
 /* A decompress chunk of at most 8 blocks, each of at least sc_lat_min (debug key, default 2048)
  * compressed bytes, decodes on one latency-decoder pipeline (the whole GPU on
@@ -619,16 +679,23 @@ static int lat_chunk(struct slot *S, const struct layout *L, const uint8_t *h, u
     for (uint32_t i = 0; i < nb; i++)
         if (!use_lat_decoder(sl[i]))
             return 0;
+    (void)S;
     const size_t need = lzo_mi355x_decompress_lat_scratch_n(so, sl, dc, nb);
-    if (need == 0 || need > kLatMaxScratch || lat_reserve(S, need) != 0)
+    if (need == 0 || need > kLatMaxScratch)
         return 0;
     uint8_t *scr = d + L->o_scr;
     uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nb));
     uint32_t *ol = (uint32_t *)(d + L->o_outlen);
     int32_t *st = (int32_t *)(d + L->o_status);
-    if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess ||
-        lzo_mi355x_launch_decompress_lat_n(d + L->o_src, so, sl, d + L->o_dst, dof, dc, nb, ol, st, fb, ids, 0,
-                                           S->lat, S->latcap, s) != 0 ||
+    if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
+        return -1;
+    struct lat_scratch *LS = lat_acquire(need, s);
+    if (!LS)
+        return 0;                               /* (the chunk's usual decoders) */
+    const int lrc = lzo_mi355x_launch_decompress_lat_n(d + L->o_src, so, sl, d + L->o_dst, dof, dc, nb, ol, st,
+                                                       fb, ids, 0, LS->buf, LS->cap, s);
+    lat_release(LS, s);
+    if (lrc != 0 ||
         lzo_mi355x_launch_decompress_exact(d + L->o_src, (const uint64_t *)(d + L->o_srcoff),
                                            (const uint32_t *)(d + L->o_srclen), d + L->o_dst,
                                            (const uint64_t *)(d + L->o_dstoff), (const uint32_t *)(d + L->o_dstcap),
@@ -1024,7 +1091,13 @@ static void sc_init(void)
 {
     for (int d = 0; d < kMaxDev; d++) {
         pthread_mutex_init(&sc_q[d].mu, NULL);
-        pthread_cond_init(&sc_q[d].cv, NULL);
+        /* the leader's ~50 us wait for company is a relative time: measure
+         * it on CLOCK_MONOTONIC, which wall-clock adjustments do not move */
+        pthread_condattr_t ca;
+        pthread_condattr_init(&ca);
+        pthread_condattr_setclock(&ca, CLOCK_MONOTONIC);
+        pthread_cond_init(&sc_q[d].cv, &ca);
+        pthread_condattr_destroy(&ca);
     }
 }
 
@@ -1095,27 +1168,6 @@ static int use_lat_decoder(size_t z)
 }
 
 
-/* The slot's latency-decoder scratch, at least `bytes`.  Called only between
- * groups, when nothing of the slot is running. */
-static int lat_reserve(struct slot *t, size_t bytes)
-{
-    if (t->latcap >= bytes)
-        return 0;
-    if (t->lat) {
-        hipStreamSynchronize(t->stream);
-        hipFree(t->lat);
-        t->lat = NULL;
-        t->latcap = 0;
-    }
-    const size_t want = ALIGN_UP(bytes + bytes / 4, (size_t)1 << 20);
-    if (hipMalloc(&t->lat, want) != hipSuccess) {
-        t->lat = NULL;
-        return -1;
-    }
-    t->latcap = want;
-    return 0;
-}
-
 /* A group of k <= 8 decodes of at least sc_lat_min compressed bytes each
  * runs as ONE latency-decoder pipeline (lzo1x_decode_lat.hip: the blocks side
  * by side in every kernel).  Returns 1 when launched, 0 when the group does
@@ -1140,11 +1192,17 @@ static int lat_group(struct slot *t, struct sc_req **g, int k, const uint8_t *d,
         z[i] = (uint32_t)g[i]->src_len;
         cap[i] = (uint32_t)g[i]->room;
     }
+    (void)t;
     const size_t need = lzo_mi355x_decompress_lat_scratch_n(so, z, cap, (uint32_t)k);
-    if (need == 0 || need > kLatMaxScratch || lat_reserve(t, need) != 0)
+    if (need == 0 || need > kLatMaxScratch)
         return 0;                               /* out of its range: the windowed decoder */
-    return lzo_mi355x_launch_decompress_lat_n(d, so, z, out, doff, cap, (uint32_t)k, olen, ost, fb, fb + 1, 0,
-                                              t->lat, t->latcap, s) == 0 ? 1 : -1;
+    struct lat_scratch *LS = lat_acquire(need, s);
+    if (!LS)
+        return 0;
+    const int rc = lzo_mi355x_launch_decompress_lat_n(d, so, z, out, doff, cap, (uint32_t)k, olen, ost, fb, fb + 1,
+                                                      0, LS->buf, LS->cap, s);
+    lat_release(LS, s);
+    return rc == 0 ? 1 : -1;
 }
 
 static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
@@ -1294,7 +1352,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
         q->leader = 1;
         if (q->last_k > 1 && q->head == q->tail) {
             struct timespec ts;
-            clock_gettime(CLOCK_REALTIME, &ts);
+            clock_gettime(CLOCK_MONOTONIC, &ts);
             ts.tv_nsec += 50000;
             if (ts.tv_nsec >= 1000000000L) {
                 ts.tv_sec++;

@@ -7,6 +7,7 @@ vectors and the oracle.  Bit-exact everywhere (integer/byte work):
 """
 from __future__ import annotations
 
+import ctypes
 import hashlib
 
 import numpy as np
@@ -817,3 +818,43 @@ def test_small_host_batches_on_the_latency_decoder(dev, oracle, malformed, k):
         assert s == want[i][0], (i, s, want[i][0])
         if s == 0:
             assert o == want[i][1], i
+
+
+def test_latency_scratch_is_shared_across_threads(dev, oracle):
+    """16 threads issuing 8-block host batches (each one latency-decoder
+    pipeline, lzo_host.c lat_chunk) share ONE latency scratch per device
+    (lat_acquire): the device memory they leave allocated stays near one
+    scratch plus the threads' staging, where per-thread scratches (round 3)
+    would hold 16 of them.  Every batch still decodes exactly."""
+    from concurrent.futures import ThreadPoolExecutor
+    blocks = [synth.block(synth.ITB, 8181 + i, 262144) for i in range(8)]
+    comps = [oracle.compress(b) for b in blocks]
+    caps = [len(b) for b in blocks]
+    lib = lzo.load()
+    lib.lzo_mi355x_decompress_lat_scratch_n.restype = ctypes.c_size_t
+    lib.lzo_mi355x_decompress_lat_scratch_n.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32]
+    so = np.zeros(8, np.uint64)
+    so[1:] = np.cumsum([(len(z) + 255) // 256 * 256 for z in comps[:-1]])
+    zl = np.array([len(z) for z in comps], np.uint32)
+    cp = np.array(caps, np.uint32)
+    need = lib.lzo_mi355x_decompress_lat_scratch_n(so.ctypes.data, zl.ctypes.data, cp.ctypes.data, 8)
+    assert need > 32 << 20                       # (a scratch worth sharing)
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+
+    def work(i):
+        for _ in range(2):
+            rc, st, outs = lzo.decompress_batch(comps, caps)
+            if rc != 0 or st != [0] * 8 or outs != blocks:
+                return False
+        return True
+
+    with ThreadPoolExecutor(16) as ex:
+        ok = list(ex.map(work, range(16)))
+    assert all(ok)
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    held = free0 - free1
+    staging = 16 * 4 * (int(zl.sum()) + int(cp.sum()) + (1 << 20))   # each thread's chunk staging, generously
+    assert held <= 2 * need + staging, (held, need, staging)
+    assert held < 16 * need, (held, need)
