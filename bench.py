@@ -84,6 +84,15 @@ def host_cores():
     return max(1, min(n, cap) if cap > 0 else n)
 
 
+def affinity_cpus():
+    """Every CPU of this process's affinity set (the CPU baseline's headline
+    thread count)."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def host_cpu_info():
     """What `cores` was taken from: the affinity set, the OMP_NUM_THREADS cap
     and the machine's logical CPUs (a GPU box is a share of a larger machine)."""
@@ -185,7 +194,7 @@ def cpu_baseline(plain, comps, seconds, roundtrip=True):
         kind = "port"
         dec = None
         comp = None
-    threads = host_cores()
+    threads = affinity_cpus()
     nsample = len(plain)
     lens = [len(p) for p in plain]
     srcs = [ctypes.create_string_buffer(comps[b], len(comps[b]) + 64) for b in range(nsample)]
@@ -233,27 +242,43 @@ def cpu_baseline(plain, comps, seconds, roundtrip=True):
             b = (b + threads) % nsample
         nbytes[t] = done
 
-    res = {}
-    for name, fn, share in (("decompress", dec_share, 0.6), ("compress", comp_share, 0.4)):
-        nbytes = [0] * threads
-        t0 = time.perf_counter()
-        deadline = t0 + seconds * share
-        with ThreadPoolExecutor(threads) as ex:
-            list(ex.map(lambda t: fn(t, deadline, nbytes), range(threads)))
-        dt = time.perf_counter() - t0
-        res[name] = sum(nbytes) / dt / GIB
-    # value: the bench metric itself -- the round trip (compress then decompress
-    # of every byte on the same cores: 1 / (1/compress + 1/decompress)), or
-    # decompress for the decode-only C2 line; both legs beside it
-    rt = 1.0 / (1.0 / res["compress"] + 1.0 / res["decompress"]) if roundtrip else res["decompress"]
-    return {"value": round(rt, 4), "unit": "GiB/s", "cores": threads,
+    def measure(nthr, secs):
+        res = {}
+        for name, fn, share in (("decompress", dec_share, 0.6), ("compress", comp_share, 0.4)):
+            nbytes = [0] * nthr
+            t0 = time.perf_counter()
+            deadline = t0 + secs * share
+            with ThreadPoolExecutor(nthr) as ex:
+                list(ex.map(lambda t: fn(t, deadline, nbytes), range(nthr)))
+            dt = time.perf_counter() - t0
+            res[name] = sum(nbytes) / dt / GIB
+        # the bench metric itself -- the round trip (compress then decompress of
+        # every byte on the same cores: 1 / (1/compress + 1/decompress)), or
+        # decompress for the decode-only C2 line; both legs beside it
+        rt = 1.0 / (1.0 / res["compress"] + 1.0 / res["decompress"]) if roundtrip else res["decompress"]
+        return {"value": round(rt, 4), "compress_value": round(res["compress"], 4),
+                "decompress_value": round(res["decompress"], 4), "seconds": round(secs, 1)}
+
+    # one thread per CPU of the affinity set (the headline), the box's
+    # OMP_NUM_THREADS share and one core beside it
+    counts = []
+    for c in (threads, host_cores(), 1):
+        if c not in counts:
+            counts.append(c)
+    by = {str(c): measure(c, seconds if c == threads else seconds / 2) for c in counts}
+    top = by[str(threads)]
+    return {"value": top["value"], "unit": "GiB/s", "cores": threads,
             "host": host_cpu_info(),
-            "kind": kind, "compress_value": round(res["compress"], 4),
-            "decompress_value": round(res["decompress"], 4),
+            "kind": kind, "compress_value": top["compress_value"],
+            "decompress_value": top["decompress_value"],
+            "by_threads": by,
+            "one_core": by["1"],
             "byte_identical_blocks": f"{identical}/{nsample}",
             "sample": f"{nsample} of the same {lens[0]}-byte ITB blocks, round-robin over "
-                      f"{threads} threads for {seconds:.0f} s (decompress {0.6 * seconds:.0f} s,"
-                      f" compress {0.4 * seconds:.0f} s), "
+                      f"{threads} threads (one per CPU of the affinity set) for {seconds:.0f} s "
+                      f"(decompress {0.6 * seconds:.0f} s, compress {0.4 * seconds:.0f} s); "
+                      f"by_threads repeats it on {', '.join(str(c) for c in counts[1:])} thread(s) for "
+                      f"{seconds / 2:.0f} s each; "
                       + ("lib/minilzo.c built from the reference sources (oracle/_ref)"
                          if kind == "reference" else "oracle/lzo1x_oracle.c port")}
 
@@ -578,6 +603,14 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
         "errors": errors,
         "fallback_blocks": R.fallback_blocks,
     }
+    # whole-job HBM fraction over every GPU of the run:
+    # algorithmic bytes of all ranks over the max-over-ranks time, against
+    # G x 8 TB/s -- decode alone, and both kernels of the round trip
+    agg = {"gpus": world, "peak_GBps_per_gpu": HBM_PEAK_GBPS,
+           "decode_frac": round((z_all + n_all) * args.steps / dec_wall / 1e9 / (world * HBM_PEAK_GBPS), 4)}
+    if args.workload == "c3":
+        agg["roundtrip_frac"] = round(2 * (z_all + n_all) * args.steps / wall / 1e9 / (world * HBM_PEAK_GBPS), 4)
+    result["aggregate_hbm"] = agg
     copy = copy_gbps(torch, dev)
     for key in ("roofline", "compress_roofline"):
         result[key]["copy_GBps_measured"] = round(copy, 1)

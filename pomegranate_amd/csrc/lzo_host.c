@@ -287,13 +287,16 @@ size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
  * (lzo1x_decode_win.hip: 2 blocks per CU, a 64 KiB LDS output ring, never
  * reads its own output back).  Debug key decoder=fast|win|seg forces one;
  * single calls always use the windowed one (see single_call). */
-enum { DEC_FAST = 0, DEC_WIN = 1, DEC_SEG = 2 };
+enum { DEC_FAST = 0, DEC_WIN = 1, DEC_SEG = 2, DEC_QUAD = 3 };
 static int use_win_decoder(uint32_t nblocks)
 {
     char buf[16];
     const char *e = pom_dbg_str("decoder", buf, sizeof buf);
     if (e)
-        return strcmp(e, "win") == 0 ? DEC_WIN : strcmp(e, "seg") == 0 ? DEC_SEG : DEC_FAST;
+        return strcmp(e, "win") == 0    ? DEC_WIN
+               : strcmp(e, "seg") == 0  ? DEC_SEG
+               : strcmp(e, "quad") == 0 ? DEC_QUAD
+                                        : DEC_FAST;
     /* default: the windowed decoder while the batch fits two workgroups per
      * CU (one round; lone blocks decode 1.3-1.5x faster there), the op-set
      * decoder for larger batches (16 blocks per CU) */
@@ -350,9 +353,10 @@ static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, cons
          * only the fallback list */
         if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
             return -1;
-        if ((win == DEC_SEG ? lzo_mi355x_launch_decompress_seg
-                            : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
-                                                                out_len, status, fb, ids, nblocks, s) != 0)
+        if ((win == DEC_SEG    ? lzo_mi355x_launch_decompress_seg
+             : win == DEC_QUAD ? lzo_mi355x_launch_decompress_quad
+                               : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
+                                                                   out_len, status, fb, ids, nblocks, s) != 0)
             return -1;
     } else {
         if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)

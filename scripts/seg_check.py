@@ -27,7 +27,7 @@ fast = lib.lzo_mi355x_launch_decompress_fast
 fast.restype = ctypes.c_int
 fast.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
 one = {}
-for k in ("seg", "ser", "win"):
+for k in ("seg", "ser", "win", "quad"):
     f = getattr(lib, f"lzo_mi355x_launch_decompress_{k}", None)
     if f is not None:
         f.restype = ctypes.c_int

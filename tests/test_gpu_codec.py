@@ -601,6 +601,51 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
     assert not bad, bad[:10]
 
 
+def _ring_blocks():
+    """Blocks for the lone-block encoder's input ring (64 KiB in LDS): larger
+    than the ring, matches at distances just under and past 0xBFFF, matches
+    longer than the ring (the extension leaves the staged bytes), zero runs,
+    random data and ITB records."""
+    rng = np.random.default_rng(5)
+    rnd = lambda k: rng.integers(0, 256, k, dtype=np.uint8).tobytes()
+    a = rnd(0xBFF0)
+    b = rnd(0xC010)
+    return [
+        _large_block((3 << 20) + 5, 3),
+        bytes(1 << 20),
+        rnd(1 << 20),
+        synth.block(synth.ITB, 7, 536192),
+        a + a + a[:5000] + rnd(3000) + a,               # distance 0xBFF0 (inside M4_MAX_OFFSET)
+        b + b + rnd(100),                               # distance 0xC010 (past it: literals)
+        rnd(70000) + bytes(200000) + rnd(10) + bytes(90000),
+        (rnd(37) * 20000)[:700001],
+        synth.block(synth.ITB, 8, 65536),
+        b"",
+        rnd(13),
+        rnd(14),
+    ]
+
+
+@pytest.mark.parametrize("which", ["sweep", "ring"])
+def test_lone_block_encoder_vs_oracle(dev, gu, oracle, which):
+    """The lone-block encoder (one workgroup per CU, LDS dictionary, block
+    staged through a 64 KiB LDS input ring; batches of at most one block per
+    CU without scratch): byte-identical to the oracle on the sweep's content
+    models and on blocks that exercise the ring."""
+    blocks = _sweep_blocks(200, 93) if which == "sweep" else _ring_blocks()
+    assert len(blocks) <= torch.cuda.get_device_properties(dev).multi_processor_count
+    src = gu.device_batch(torch, blocks, dev, shift=3)
+    dst = gu.empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
+    olen = torch.zeros(len(blocks), dtype=torch.int32, device=dev)
+    st = torch.full((len(blocks),), 99, dtype=torch.int32, device=dev)
+    lzo.compress_dev(src, dst, olen, st, scratch=None)
+    torch.cuda.synchronize()
+    assert st.cpu().numpy().tolist() == [0] * len(blocks)
+    comps = gu.fetch(dst, olen)
+    bad = [i for i, (b, c) in enumerate(zip(blocks, comps)) if c != oracle.compress(b)]
+    assert not bad, bad[:10]
+
+
 @pytest.mark.gpu
 def test_encoder_block_tickets_mixed_sizes(dev, gu):
     """More blocks than the global-dictionary grid, of mixed ITB sizes (C4's
@@ -641,7 +686,7 @@ def test_encoder_block_tickets_mixed_sizes(dev, gu):
     assert torch.equal(back, src.arena)
 
 
-@pytest.mark.parametrize("kind", ["win", "seg"])
+@pytest.mark.parametrize("kind", ["win", "seg", "quad"])
 def test_window_decoder_every_valid_stream(dev, gu, kind):
     """The windowed (lzo1x_decode_win.hip) and table-walk
     (lzo1x_decode_ser.hip) decoders alone, without the exact decoder behind it: every content model (incompressible blocks with
@@ -667,7 +712,7 @@ def test_window_decoder_every_valid_stream(dev, gu, kind):
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("kind", ["win", "seg"])
+@pytest.mark.parametrize("kind", ["win", "seg", "quad"])
 def test_window_decoder_full_grammar_streams(dev, gu, kind):
     """LZO1X streams the LZO1X-1 compressor never writes (M1 after literal runs
     and trailing literals, long extensions, first runs of 1-3 bytes) decode
@@ -683,7 +728,7 @@ def test_window_decoder_full_grammar_streams(dev, gu, kind):
     assert outs == want
 
 
-@pytest.mark.parametrize("kind", ["win", "seg"])
+@pytest.mark.parametrize("kind", ["win", "seg", "quad"])
 def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, kind, malformed):
     """Malformed streams, and valid streams whose output does not fit, are
     handed to the exact decoder (status 0x7FFF0001 until it runs) -- never
