@@ -127,10 +127,12 @@ struct Tok {
     uint32_t fl;         // TK_*
 };
 
+constexpr uint32_t kMaxExtZeros = 64;            // zero length-extension bytes a lane reads at most
+
 // One instruction at (pos, st), general form: long length extensions and
 // instructions that run past the staged piece (bytes read from HBM).  Bytes
 // at or past z read as 0 and make the instruction TK_BAD.
-__device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t pos, uint32_t st)
+__device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t pos, uint32_t st, bool spec)
 {
     Tok r;
     r.aL = r.bL = r.aS = r.bS = 0;
@@ -140,11 +142,20 @@ __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t po
         far = p + 1 > far ? p + 1 : far;
         return p < k.z ? in_byte(L, k, p) : 0u;
     };
+    // (spec: a lane decoding speculatively from inside a long zero run would
+    // scan the rest of it, for every start in the run; after kMaxExtZeros zero
+    // bytes its guess is refused instead.  The true path -- the frontier,
+    // counting and emitting walks -- scans each run once: linear time)
+    bool capped = false;
     auto ext = [&](uint32_t& p, uint32_t base) -> uint32_t {
         uint32_t v = 0;
         while (p < k.z && rd(p) == 0) {
             v += 255;
             p++;
+            if (spec && v > 255u * kMaxExtZeros) {
+                capped = true;
+                break;
+            }
         }
         v += base + rd(p);
         p++;
@@ -222,8 +233,8 @@ __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t po
 done:
     {
         const uint32_t need = far > r.pos ? far : r.pos;
-        if (need > k.z || r.pos < pos)
-            r.fl = TK_BAD;                       // runs past the input (INPUT_OVERRUN)
+        if (need > k.z || r.pos < pos || capped)
+            r.fl = TK_BAD;                       // runs past the input (INPUT_OVERRUN), or a capped zero run
         else if ((r.fl & TK_EOF) && r.pos != k.z)
             r.fl = TK_BAD;                       // EOF not at the end (INPUT_NOT_CONSUMED)
     }
@@ -233,7 +244,7 @@ done:
 // Branch-free form for the common case: the instruction's fields lie in its
 // first 4 bytes (no 255-chunk length extension) inside the staged piece.
 // One zin round trip.
-__device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos, uint32_t st)
+__device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos, uint32_t st, bool spec = false)
 {
     const uint32_t off = k.zb + (pos - k.I);
     const uint32_t lo = __builtin_amdgcn_alignbyte(L.zin[(off >> 2) + 1], L.zin[off >> 2], off & 3u);
@@ -247,7 +258,7 @@ __device__ __forceinline__ Tok tok(const WinLds& L, const Piece& k, uint32_t pos
     const bool m4 = !flit && t >= 16 && t < 32;
     const bool ext = (lit && t == 0) || (m3 && (t & 31) == 0) || (m4 && (t & 7) == 0);
     if (__builtin_expect((ext && b1 == 0) || pos + 4 > k.sEnd, 0))
-        return tok_slow(L, k, pos, st);
+        return tok_slow(L, k, pos, st, spec);
     const uint32_t e = ext ? 1u : 0u;
     const uint32_t o16 = __builtin_amdgcn_ubfe(lo, 8u + 8u * e, 16);
     const uint32_t dd4 = ((t & 8u) << 11) + (o16 >> 2);
@@ -357,7 +368,7 @@ __device__ PieceOut parse_piece(WinLds& L, const Blk& blk, uint32_t I, uint32_t 
             uint32_t st = j ? (uint32_t)ST_A : st_in;
             uint32_t restart = pos;
             while (pos < b) {
-                const Tok t = tok(L, k, pos, st);
+                const Tok t = tok(L, k, pos, st, j != 0);   // (lane 0 starts at the true entry)
                 if (t.fl) {
                     if (j == 0 || (t.fl & TK_EOF))
                         break;                   // stop point

@@ -286,143 +286,6 @@ __device__ uint32_t extend_match(const BlockSrc& B, uint32_t n, uint32_t mc, uin
 }
 
 // ---------------------------------------------------------------------------
-// Input ring (lone-block encoder, lzo1x_encode_ring_kernel): the block's bytes
-// staged in LDS by a loader wave, so the parse wave's probe-word, candidate
-// and first extension reads are LDS round trips instead of L2 ones.  Byte x
-// lives at ring[x mod kRingB]; a 64-byte mirror past the end keeps reads that
-// cross it contiguous.  The loader stages 1 KiB chunks ahead of the parse,
-// overwriting only positions more than M4_MAX_OFFSET behind the window the
-// parse wave last published -- no candidate can reach them
-// (lib/minilzo.c:2878-2883).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kRingB = 65536;
-constexpr uint32_t kRingMask = kRingB - 1;
-constexpr uint32_t kRingChunk = 1024;
-constexpr uint32_t kRingDone = 0x7FFF0000u;      // published window start once the parse is done
-struct RingIn {
-    uint8_t* ring;                                  // LDS, kRingB + 64 bytes
-    uint32_t* staged;                               // LDS: positions below it are in the ring
-    uint32_t* pub;                                  // LDS: the parse wave's window start
-    uint32_t full;                                  // the loader stops here
-    uint32_t stg;                                   // (parse wave) last value of *staged seen
-};
-
-typedef uint32_t v4u32e __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t lds_addr(const void* p)
-{
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-// 8 dwords from LDS byte address a (any alignment: gfx950 runs LDS in
-// unaligned mode, scripts/probe/lds_misaligned_probe.hip), and 2 x 8 dwords.
-__device__ __forceinline__ void lds_read32(uint32_t a, uint32_t (&w)[8])
-{
-    v4u32e x, y;
-    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(x), "=&v"(y) : "v"(a) : "memory");
-    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-    w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-}
-__device__ __forceinline__ void lds_read32x2(uint32_t a, uint32_t b, uint32_t (&w)[8], uint32_t (&u)[8])
-{
-    v4u32e x, y, z, t;
-    asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\t"
-                 "ds_read_b128 %2, %5\n\tds_read_b128 %3, %5 offset:16\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(x), "=&v"(y), "=&v"(z), "=&v"(t) : "v"(a), "v"(b) : "memory");
-    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-    w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-    u[0] = z.x; u[1] = z.y; u[2] = z.z; u[3] = z.w;
-    u[4] = t.x; u[5] = t.y; u[6] = t.z; u[7] = t.w;
-}
-__device__ __forceinline__ uint32_t lds_read4(uint32_t a)
-{
-    uint32_t x;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(a) : "memory");
-    return x;
-}
-// The parse wave waits until the ring holds every position below x.
-__device__ __forceinline__ void ring_ensure(RingIn& R, uint32_t x)
-{
-    x = x < R.full ? x : R.full;
-    while (R.stg < x) {
-        __builtin_amdgcn_s_sleep(1);
-        R.stg = __builtin_amdgcn_readfirstlane(lds_load(R.staged));
-    }
-}
-
-// extend_match with the ring: rounds whose bytes are staged read LDS, later
-// ones the block in memory (a match may run past what the ring can hold).
-__device__ uint32_t extend_match_ring(const BlockSrc& B, RingIn& R, uint32_t n, uint32_t mc, uint32_t mp,
-                                      uint32_t k0, uint32_t l)
-{
-    const uint32_t lim = n - mp;
-    const uint32_t rb = lds_addr(R.ring);
-    for (uint32_t k = k0;; k += 4 * kWave) {
-        const uint32_t idx = k + 4 * l;
-        const uint32_t hi = mp + k + 4 * kWave + 4;
-        if (R.stg < hi && R.stg < R.full)
-            R.stg = __builtin_amdgcn_readfirstlane(lds_load(R.staged));
-        uint32_t a, b;
-        if (hi <= R.stg) {
-            a = lds_read4(rb + ((mc + idx) & kRingMask));
-            b = lds_read4(rb + ((mp + idx) & kRingMask));
-        } else {
-            uint32_t x[1], y[1];
-            load_at<1>(B, mc + idx, x);
-            load_at<1>(B, mp + idx, y);
-            a = x[0];
-            b = y[0];
-        }
-        const uint32_t x = a ^ b;
-        uint32_t e = idx < lim && x ? idx + ((uint32_t)__builtin_ctz(x) >> 3) : 0xFFFFFFFFu;
-        if (idx + 4 > lim)
-            e = e < lim ? e : lim;
-        const uint64_t mis = wave_ballot(e != 0xFFFFFFFFu);
-        if (mis)
-            return lane_read(e, (uint32_t)__builtin_ctzll(mis));
-    }
-}
-
-// Loader wave: stages the block into the ring, up to 4 KiB per round trip.
-__device__ void ring_load_wave(const RingIn R, const uint8_t* in, uint32_t n, uint32_t l)
-{
-    const BlockSrc B = block_src(in, n);
-    const uint32_t rb = lds_addr(R.ring);
-    for (uint32_t st = 0; st < R.full;) {
-        const uint32_t ipp = __builtin_amdgcn_readfirstlane(lds_load(R.pub));
-        if (ipp == kRingDone)
-            break;
-        // positions st .. st + c*1K - 1 overwrite st - kRingB ..: all of them
-        // must lie below ipp - M4_MAX_OFFSET
-        const uint32_t lim = ipp + kRingB - (kM4MaxOffset + 1);
-        uint32_t c = lim > st ? (lim - st) / kRingChunk : 0u;
-        c = c < 4u ? c : 4u;
-        const uint32_t left = (R.full - st) / kRingChunk;
-        c = c < left ? c : left;
-        if (c == 0) {
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        uint32_t w[4][4];
-#pragma unroll
-        for (uint32_t i = 0; i < 4; i++)
-            if (i < c)
-                load_at<4>(B, st + i * kRingChunk + 16 * l, w[i]);
-#pragma unroll
-        for (uint32_t i = 0; i < 4; i++)
-            if (i < c) {
-                const uint32_t o = (st + i * kRingChunk + 16 * l) & kRingMask;
-                const v4u32e v = {w[i][0], w[i][1], w[i][2], w[i][3]};
-                asm volatile("ds_write_b128 %0, %1" : : "v"(rb + o), "v"(v) : "memory");
-                if (o < 64)
-                    asm volatile("ds_write_b128 %0, %1" : : "v"(rb + kRingB + o), "v"(v) : "memory");
-            }
-        __builtin_amdgcn_s_waitcnt(0xC07F);             // lgkmcnt(0): the chunks are in LDS
-        st += c * kRingChunk;
-        lds_store(R.staged, st);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Emitter: tokens -> the LZO1X byte stream (lzo1x_emit.h) in an LDS ring,
 // stored to HBM.  Run by the emit wave (two-wave kernels) or, in the fused
 // kernel, by the parse wave itself after each window.
@@ -628,9 +491,9 @@ constexpr int kEncStampSlots = 16;
 #ifndef POM_ENC_DRAIN
 #define POM_ENC_DRAIN 32
 #endif
-template <bool STAMPS, bool GD, bool FUSED = false, bool RING = false>
+template <bool STAMPS, bool GD, bool FUSED = false>
 __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, uint32_t n, uint32_t l,
-                           uint64_t* acc, Emitter<GD>* E = nullptr, RingIn* R = nullptr)
+                           uint64_t* acc, Emitter<GD>* E = nullptr)
 {
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
 #define ESTAMP(ph)                                                  \
@@ -698,9 +561,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
         // read as soon as its start is known, ahead of the token and
         // dictionary writes.
         uint32_t pw[kCmpW];
-        const uint32_t rb = RING ? lds_addr(R->ring) : 0u;
-        if (!RING)
-            load_at<kCmpW>(B, ip + l, pw);
+        load_at<kCmpW>(B, ip + l, pw);
         ESTAMP(EP_SETUP);
         for (;;) {
             if (STAMPS)
@@ -736,14 +597,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 wave_order();
                 base = nb;
             }
-            if (RING) {
-                // publish the window (the loader may drop what lies more than
-                // M4_MAX_OFFSET before it), then its probe words from the ring
-                lds_store(R->pub, ip);
-                ring_ensure(*R, ip + kWave + 4 * kCmpW + 4);
-                static_assert(kCmpW == 8, "ring probe-word reads are 32 bytes");
-                lds_read32(rb + ((ip + l) & kRingMask), pw);
-            } else if (POM_ENC_AHEAD) {
+            if (POM_ENC_AHEAD) {
                 if (FUSED)
                     prefetch(ip);
                 else
@@ -769,9 +623,6 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
             const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
             uint32_t c1w[kCmpW], c2w[kCmpW];        // (read unconditionally; used only if valid)
-            if (RING) {
-                lds_read32x2(rb + (w1 & kRingMask), rb + (w2 & kRingMask), c1w, c2w);
-            } else {
 #if POM_ENC_FARINV
             // (lanes without a valid candidate read past the block: range
             // checked, no memory request; the secondary candidate is only
@@ -783,7 +634,6 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             load_at<kCmpW>(B, w1, c1w);
             load_at<kCmpW>(B, w2, c2w);
 #endif
-            }
             const uint32_t b3 = pw[0] >> 24;
             // (selects, no branches)
             const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
@@ -835,8 +685,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                     if (len == kCmpB && n - (ip + q) > kCmpB) {
                         if (STAMPS)
                             acc[EC_EXTEND] += 1;
-                        len = RING ? extend_match_ring(B, *R, n, lane_read(cand, q), ip + q, kCmpB, l)
-                                   : extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
+                        len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
                         if (STAMPS)
                             acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
                         mlen = l == q ? len : mlen;
@@ -922,8 +771,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
 
             uint32_t npw[kCmpW];
-            if (!RING)
-                load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
+            load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
 
             ESTAMP(EP_CLAIM);
             // ---- tokens for the matches before the cut ------------------------
@@ -980,15 +828,11 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             ip += end;
             if (ip >= ip_end)
                 break;
-            if (!RING) {
 #pragma unroll
-                for (int i = 0; i < kCmpW; i++)
-                    pw[i] = npw[i];
-            }
+            for (int i = 0; i < kCmpW; i++)
+                pw[i] = npw[i];
         }
     }
-    if (RING)
-        lds_store(R->pub, kRingDone);                // (the loader stops)
     push(ii, n - ii, 0, 0);                          // tail + EOF
     if (FUSED) {
         E->drain(tp);                                // through the tail: out_len, status set
@@ -1181,63 +1025,6 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
     }
 }
 
-// Lone-block encoder: one workgroup per CU, three waves -- parse (LDS
-// dictionary, input from the LDS ring), emit, and the ring loader.  For
-// batches of at most one block per CU (single calls, small host chunks): a
-// block's window chain then waits on LDS instead of L2 round trips.
-struct __attribute__((aligned(16))) EncRingLds {
-    EncLdsT<false> e;
-    uint8_t ring[kRingB + 64];
-    uint32_t staged;
-};
-static_assert(sizeof(EncRingLds) <= 160 * 1024, "LDS budget");
-
-__global__ __launch_bounds__(3 * kWave) void lzo1x_encode_ring_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
-    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks)
-{
-    __shared__ EncRingLds S;
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks)
-        return;
-    const uint32_t n = src_len[b];
-    if (n > kMaxN) {
-        if (threadIdx.x == 0)
-            status[b] = LZO_MI355X_ENC_PENDING;
-        return;
-    }
-    const uint32_t l = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (threadIdx.x == 0) {
-        S.e.prod = 0;
-        S.e.cons = 0;
-        S.e.ip = 0;
-        S.staged = 0;
-    }
-    __syncthreads();
-    const uint8_t* in = src + src_off[b];
-    RingIn R;
-    R.ring = S.ring;
-    R.staged = &S.staged;
-    R.pub = &S.e.ip;
-    // every read of the parse lies below n + 100 (probe words of the last window)
-    R.full = (n + kWave + 4 * kCmpW + 4 + kRingChunk - 1) / kRingChunk * kRingChunk;
-    R.stg = 0;
-    if (wave == 0) {
-        Dict<false> D;
-        D.lds = S.e.dict;
-        D.g = nullptr;
-        uint64_t acc[EP_N];
-        parse_wave<false, false, false, true>(S.e, D, in, n, l, acc, nullptr, &R);
-    } else if (wave == 1) {
-        emit_wave<false>(S.e, in, n, dst + dst_off[b], dst_cap[b], out_len, status, b);
-    } else {
-        ring_load_wave(R, in, n, l);
-    }
-}
-
 }  // namespace
 
 // Waves per block of the global-dictionary encoder: debug key enc_waves of
@@ -1248,24 +1035,19 @@ static int enc_waves(void)
     return pom_dbg_int("enc_waves", 1) == 2 ? 2 : 1;
 }
 
-static uint32_t enc_cus(void)
+static uint32_t enc_resident(void)
 {
     static int cus[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-        return 256;
+        return 256 * POM_ENC_RESIDENT;
     if (!cus[dev]) {
         int n = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
             n = 256;
         cus[dev] = n;
     }
-    return (uint32_t)cus[dev];
-}
-
-static uint32_t enc_resident(void)
-{
-    return enc_cus() * (enc_waves() == 1 ? POM_ENC_RESIDENT1 : POM_ENC_RESIDENT);
+    return (uint32_t)cus[dev] * (enc_waves() == 1 ? POM_ENC_RESIDENT1 : POM_ENC_RESIDENT);
 }
 
 // Grid of the global-dictionary encoders: one workgroup per dictionary region
@@ -1298,10 +1080,7 @@ extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_
     const uint32_t grid = scratch ? enc_grid(scratch_bytes, nblocks) : 0u;
     if (grid && grid < nblocks && hipMemsetAsync(scratch, 0, sizeof(uint32_t), stream) != hipSuccess)
         return -1;                                   // (the block ticket)
-    if (!grid && nblocks <= enc_cus() && pom_dbg_int("enc_ring", 1))
-        hipLaunchKernelGGL(lzo1x_encode_ring_kernel, dim3(nblocks), dim3(3 * kWave), 0, stream, src, src_off,
-                           src_len, dst, dst_off, dst_cap, out_len, status, nblocks);
-    else if (grid && enc_waves() == 1)
+    if (grid && enc_waves() == 1)
         hipLaunchKernelGGL(lzo1x_encode_gdict1_kernel, dim3(grid), dim3(kWave), 0, stream, src, src_off,
                            src_len, dst, dst_off, dst_cap, out_len, status, nblocks, (uint8_t*)scratch);
     else if (grid)

@@ -29,7 +29,7 @@
 
 /* Debug and experiment switches: ONE environment variable, POM_LZO_DEBUG,
  * a comma-separated list of key=value.  No product path
- * needs it; an unset key takes its default.  Keys: decoder=fast|seg|win
+ * needs it; an unset key takes its default.  Keys: decoder=fast|win
  * (device batches), sc_copy=1, sc_combine=0, sc_lat=0, sc_lat_min=BYTES,
  * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, enc_lds_max=N, enc_waves=1|2,
  * enc_grid=N.  Read at every use (tests change it between calls). */
@@ -285,18 +285,15 @@ size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
 /* Which throughput decoder a batch uses: the op-set decoder
  * (lzo1x_decode_fast.hip: 16 blocks per CU) or the windowed one
  * (lzo1x_decode_win.hip: 2 blocks per CU, a 64 KiB LDS output ring, never
- * reads its own output back).  Debug key decoder=fast|win|seg forces one;
+ * reads its own output back).  Debug key decoder=fast|win forces one;
  * single calls always use the windowed one (see single_call). */
-enum { DEC_FAST = 0, DEC_WIN = 1, DEC_SEG = 2, DEC_QUAD = 3 };
+enum { DEC_FAST = 0, DEC_WIN = 1 };
 static int use_win_decoder(uint32_t nblocks)
 {
     char buf[16];
     const char *e = pom_dbg_str("decoder", buf, sizeof buf);
     if (e)
-        return strcmp(e, "win") == 0    ? DEC_WIN
-               : strcmp(e, "seg") == 0  ? DEC_SEG
-               : strcmp(e, "quad") == 0 ? DEC_QUAD
-                                        : DEC_FAST;
+        return strcmp(e, "win") == 0 ? DEC_WIN : DEC_FAST;
     /* default: the windowed decoder while the batch fits two workgroups per
      * CU (one round; lone blocks decode 1.3-1.5x faster there), the op-set
      * decoder for larger batches (16 blocks per CU) */
@@ -349,14 +346,12 @@ static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, cons
     const uint32_t nsets = (uint32_t)scr_sets(nblocks);
     uint32_t *fb = (uint32_t *)scr, *ids = (uint32_t *)(scr + scr_head(nblocks));
     if (win) {
-        /* the windowed (DEC_WIN) or segment-row (DEC_SEG) decoder: no op sets,
+        /* the windowed decoder: no op sets,
          * only the fallback list */
         if (hipMemsetAsync(scr, 0, 256, s) != hipSuccess)
             return -1;
-        if ((win == DEC_SEG    ? lzo_mi355x_launch_decompress_seg
-             : win == DEC_QUAD ? lzo_mi355x_launch_decompress_quad
-                               : lzo_mi355x_launch_decompress_win)(src, src_off, src_len, dst, dst_off, dst_cap,
-                                                                   out_len, status, fb, ids, nblocks, s) != 0)
+        if (lzo_mi355x_launch_decompress_win(src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, fb,
+                                             ids, nblocks, s) != 0)
             return -1;
     } else {
         if (hipMemsetAsync(scr, 0, SCR_RING + 8 * (size_t)nsets, s) != hipSuccess)

@@ -81,23 +81,6 @@ int lzo_mi355x_launch_decompress_win(const uint8_t *src, const uint64_t *src_off
                                      uint32_t *out_len, int32_t *status, uint32_t *fallback,
                                      uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
 
-/* Segment-row throughput decoder (lzo1x_decode_seg.hip): one wave per block,
- * an 8 KiB LDS output ring, 16 blocks per CU.  Fallback list as above. */
-int lzo_mi355x_launch_decompress_seg(const uint8_t *src, const uint64_t *src_off,
-                                     const uint32_t *src_len, uint8_t *dst,
-                                     const uint64_t *dst_off, const uint32_t *dst_cap,
-                                     uint32_t *out_len, int32_t *status, uint32_t *fallback,
-                                     uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
-
-/* Quarter-wave throughput decoder (lzo1x_decode_quad.hip): four blocks per
- * workgroup (16 lanes each; parser, executor and loader waves), 8 KiB LDS
- * output ring per block, 16 blocks per CU.  Fallback list as above. */
-int lzo_mi355x_launch_decompress_quad(const uint8_t *src, const uint64_t *src_off,
-                                      const uint32_t *src_len, uint8_t *dst,
-                                      const uint64_t *dst_off, const uint32_t *dst_cap,
-                                      uint32_t *out_len, int32_t *status, uint32_t *fallback,
-                                      uint32_t *fallback_ids, uint32_t nblocks, hipStream_t stream);
-
 /* Latency decoder (lzo1x_decode_lat.hip): ONE block of z compressed bytes
  * into out (capacity cap) by a pipeline of grid-wide kernels; out_len[b] /
  * status[b] and the fallback list as above.  scratch: at least

@@ -1,7 +1,8 @@
-"""Lone-block compress latency on one GPU: the lone-block ring encoder
-(lzo1x_encode_ring_kernel) against the LDS-dictionary encoder
-(POM_LZO_DEBUG=enc_ring=0) and the global-dictionary one; kernel time by HIP
-events, outputs compared between the kernels.  Cases: one 12,416 / 65,536 /
+"""Lone-block compress latency on one GPU: the LDS-dictionary encoder
+(compress_dev without scratch, what single calls launch) against the
+global-dictionary one; kernel time by HIP events, outputs compared between
+the kernels.  (A lone-block encoder with an LDS input ring measured slower
+than the LDS-dictionary one: scripts/experiments/encode_ring.patch)  Cases: one 12,416 / 65,536 /
 536,192 B ITB record, and 256 C5-like records (12-536 KB) in one launch.
 
     python scripts/enc_lone.py [reps]"""
@@ -30,7 +31,7 @@ def case(sizes, reps):
     za = torch.zeros(int(zo[-1]) + int(caps[-1]) + 256, dtype=torch.uint8, device=dev)
     zb = lzo.DeviceBatch(za, t(zo.view(np.int64)), t(caps.view(np.int32)))
     res, outs = {}, {}
-    for name, dbg, scr in (("ring", "", None), ("lds", "enc_ring=0", None), ("gdict1", "", "auto")):
+    for name, dbg, scr in (("lds", "", None), ("gdict1", "", "auto")):
         os.environ["POM_LZO_DEBUG"] = dbg
         zl = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
         zs = torch.full_like(zl, 99)

@@ -92,6 +92,7 @@ struct __attribute__((aligned(16))) QuadLds {
     uint32_t far_done[kQ];                       // loader -> executor, parser: far records copied
     uint32_t pip[kQ];                            // parser: gen << 24 | ip (kIpDone: block parsed)
     uint32_t stg[kQ];                            // loader: gen << 24 | input bytes staged
+    uint32_t bq[kQ][4];                          // parser -> others: block of generation g (at g mod 4)
     uint32_t live;                               // waves still running (exit of the loader)
 };
 static_assert(sizeof(QuadLds) * 4 <= 160 * 1024, "four workgroups (16 blocks) per CU");
@@ -268,12 +269,11 @@ __device__ __forceinline__ void close_block(uint32_t b, bool ok, uint32_t len, u
     }
 }
 
-// Block of quarter q of workgroup w at generation g (grid stride over the
-// batch: every wave of the workgroup derives the same sequence).
-__device__ __forceinline__ uint32_t block_of(uint32_t g, uint32_t w, uint32_t q)
-{
-    return (g * gridDim.x + w) * kQ + q;
-}
+// Blocks: quarter q of workgroup w starts with block w * 4 + q; each next
+// one is a ticket the parser draws from a counter in the caller's scratch
+// (fallback[1], zero on entry) and passes to the other waves through
+// S.bq[q][g mod 4] -- quarters that drew small blocks take more of them, so a
+// batch of mixed sizes (C4: 4-256 KiB) finishes together.
 
 struct Args {
     const uint8_t* src;
@@ -338,7 +338,7 @@ __device__ void parser_wave(QuadLds& S, const Args& A)
     const uint32_t stgb = lds_off(S.stage[q]);
     const bool lead = j == 0;                    // the quarter's lane for records and counters
 
-    uint32_t g = 0, b = block_of(0, w, q);
+    uint32_t g = 0, b = w * kQ + q;
     Blk k = blk_info(b, A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
     uint32_t ph = b < A.nblocks ? (k.ok ? PH_DEC : PH_END) : PH_FIN;
     bool err = !k.ok;
@@ -588,10 +588,18 @@ __device__ void parser_wave(QuadLds& S, const Args& A)
             if (any(can)) {
                 if (can && lead)
                     S.rec[q][rcnt % kRec] = make_uint2(op | ((err ? RK_ERR : RK_END) << 24), 0);
+                // the next block: a ticket (one atomic per quarter), passed on in bq
+                uint32_t tk = 0;
+                if (can && lead)
+                    tk = atomicAdd(&A.fallback[1], 1u);
+                tk = (uint32_t)__shfl((int)tk, (int)(q * kQL), (int)kWave);
                 if (can) {
                     rcnt++;
                     g++;
-                    b = block_of(g, w, q);
+                    b = gridDim.x * kQ + tk;
+                    b = b < A.nblocks ? b : A.nblocks;
+                    if (lead)
+                        S.bq[q][g & 3] = b;
                     k = blk_info(b, A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
                     err = !k.ok;
                     ph = b < A.nblocks ? (k.ok ? PH_DEC : PH_END) : PH_FIN;
@@ -633,7 +641,7 @@ __device__ void executor_wave(QuadLds& S, const Args& A)
     const uint32_t ringb = lds_off(S.ring[q]);
     const bool lead = j == 0;
 
-    uint32_t g = 0, b = block_of(0, w, q);
+    uint32_t g = 0, b = w * kQ + q;
     Blk k = blk_info(b, A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
     bool fin = b >= A.nblocks;
     uint32_t head = 0, pass = 0, fseen = 0;      // records consumed, pass offset in the record, far records passed
@@ -766,7 +774,7 @@ __device__ void executor_wave(QuadLds& S, const Args& A)
                 if (end) {
                     head++;
                     g++;
-                    b = block_of(g, w, q);
+                    b = S.bq[q][g & 3];              // (written before the END record was published)
                     k = blk_info(b, A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
                     fin = b >= A.nblocks;
                     pos = stored = drained = pass = 0;
@@ -804,7 +812,7 @@ __device__ void loader_wave(QuadLds& S, const Args& A)
     const bool lead = j == 0;
 
     uint32_t lg = 0, ld = 0;                     // staging: generation, bytes staged
-    Blk k = blk_info(block_of(0, w, q), A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
+    Blk k = blk_info(w * kQ + q, A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
     uint32_t fdone = 0;                          // far records copied
     uint32_t fg = 0xFFFFFFFFu;                   // generation of the far block cached in fk
     Blk fk = k;
@@ -824,7 +832,7 @@ __device__ void loader_wave(QuadLds& S, const Args& A)
         if (pg != (lg & 0xFFu) && pip != (0xFF000000u | kIpDone)) {
             lg++;
             ld = 0;
-            k = blk_info(block_of(lg, w, q), A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
+            k = blk_info(S.bq[q][lg & 3], A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off, A.dst_cap);
             progress = true;
         }
         const bool pdone = (pip & 0xFFFFFFu) == kIpDone || pg != (lg & 0xFFu);
@@ -854,7 +862,7 @@ __device__ void loader_wave(QuadLds& S, const Args& A)
                 while ((gg & 0xFFu) != fgen)
                     gg++;
                 fg = gg;
-                fk = blk_info(block_of(fg, w, q), A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off,
+                fk = blk_info(S.bq[q][fg & 3], A.nblocks, A.src, A.src_off, A.src_len, A.dst, A.dst_off,
                               A.dst_cap);
             }
         }
@@ -912,6 +920,7 @@ __global__ __launch_bounds__(3 * kWave, 3) void lzo1x_decode_quad_kernel(
     __shared__ QuadLds S;
     const uint32_t t = threadIdx.x;
     if (t < kQ) {
+        S.bq[t][0] = blockIdx.x * kQ + t;
         S.rec_pub[t] = S.rec_head[t] = S.far_pub[t] = S.far_done[t] = 0;
         S.expos[t] = S.flushed[t] = 0;
         S.pip[t] = 0;

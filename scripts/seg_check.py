@@ -29,6 +29,9 @@ fast.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctyp
 one = {}
 for k in ("seg", "ser", "win", "quad"):
     f = getattr(lib, f"lzo_mi355x_launch_decompress_{k}", None)
+    xp = os.path.join(ROOT, "scripts", "experiments", f"libdecode_{k}.so")
+    if f is None and os.path.exists(xp):           # (rejected decoders: scripts/experiments)
+        f = getattr(ctypes.CDLL(xp), f"lzo_mi355x_launch_decompress_{k}", None)
     if f is not None:
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]

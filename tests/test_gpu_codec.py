@@ -601,11 +601,11 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
     assert not bad, bad[:10]
 
 
-def _ring_blocks():
-    """Blocks for the lone-block encoder's input ring (64 KiB in LDS): larger
-    than the ring, matches at distances just under and past 0xBFFF, matches
-    longer than the ring (the extension leaves the staged bytes), zero runs,
-    random data and ITB records."""
+def _far_blocks():
+    """Blocks larger than the encoder's 64 KiB position window (its u16
+    dictionary entries re-base), matches at distances just under and past
+    0xBFFF, matches longer than 64 KiB, zero runs, random data and ITB
+    records."""
     rng = np.random.default_rng(5)
     rnd = lambda k: rng.integers(0, 256, k, dtype=np.uint8).tobytes()
     a = rnd(0xBFF0)
@@ -626,13 +626,13 @@ def _ring_blocks():
     ]
 
 
-@pytest.mark.parametrize("which", ["sweep", "ring"])
-def test_lone_block_encoder_vs_oracle(dev, gu, oracle, which):
-    """The lone-block encoder (one workgroup per CU, LDS dictionary, block
-    staged through a 64 KiB LDS input ring; batches of at most one block per
-    CU without scratch): byte-identical to the oracle on the sweep's content
-    models and on blocks that exercise the ring."""
-    blocks = _sweep_blocks(200, 93) if which == "sweep" else _ring_blocks()
+@pytest.mark.parametrize("which", ["sweep", "far"])
+def test_small_batches_on_the_lds_encoder_vs_oracle(dev, gu, oracle, which):
+    """Batches without scratch of at most one block per CU (what single calls
+    and small host chunks launch: the LDS-dictionary encoder): byte-identical
+    to the oracle on the sweep's content models and on blocks with far
+    repeats around 0xBFFF, long matches and re-based dictionaries."""
+    blocks = _sweep_blocks(200, 93) if which == "sweep" else _far_blocks()
     assert len(blocks) <= torch.cuda.get_device_properties(dev).multi_processor_count
     src = gu.device_batch(torch, blocks, dev, shift=3)
     dst = gu.empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
@@ -686,7 +686,7 @@ def test_encoder_block_tickets_mixed_sizes(dev, gu):
     assert torch.equal(back, src.arena)
 
 
-@pytest.mark.parametrize("kind", ["win", "seg", "quad"])
+@pytest.mark.parametrize("kind", ["win"])
 def test_window_decoder_every_valid_stream(dev, gu, kind):
     """The windowed (lzo1x_decode_win.hip) and table-walk
     (lzo1x_decode_ser.hip) decoders alone, without the exact decoder behind it: every content model (incompressible blocks with
@@ -712,7 +712,7 @@ def test_window_decoder_every_valid_stream(dev, gu, kind):
     assert not bad, bad[:8]
 
 
-@pytest.mark.parametrize("kind", ["win", "seg", "quad"])
+@pytest.mark.parametrize("kind", ["win"])
 def test_window_decoder_full_grammar_streams(dev, gu, kind):
     """LZO1X streams the LZO1X-1 compressor never writes (M1 after literal runs
     and trailing literals, long extensions, first runs of 1-3 bytes) decode
@@ -728,7 +728,7 @@ def test_window_decoder_full_grammar_streams(dev, gu, kind):
     assert outs == want
 
 
-@pytest.mark.parametrize("kind", ["win", "seg", "quad"])
+@pytest.mark.parametrize("kind", ["win"])
 def test_window_decoder_hands_over_malformed_and_short_room(dev, gu, kind, malformed):
     """Malformed streams, and valid streams whose output does not fit, are
     handed to the exact decoder (status 0x7FFF0001 until it runs) -- never
@@ -753,8 +753,8 @@ def test_latency_decoder_valid_streams(dev, gu, group):
     """The latency decoder (lzo1x_decode_lat.hip) alone, one block per
     pipeline and eight side by side: every content model, ITB blocks up to the 536,192-byte maximum, a
     1 MiB block and the full-grammar streams (M1 after runs and trailing
-    literals, long extensions, first runs of 1-3 bytes) decode bit-exactly,
-    none handed over."""
+    literals, long extensions, first runs of 1-3 bytes) decode bit-exactly;
+    only streams with 64+ zero length-extension bytes are handed over."""
     import lzo_streams
     blocks = [synth.block(synth.ITB, 7100 + i, n)
               for i, n in enumerate((4096, 65536, 100000, 262144, 536192))]
@@ -767,9 +767,15 @@ def test_latency_decoder_valid_streams(dev, gu, group):
     comps += [z for z, _ in streams]
     want = blocks + [o for _, o in streams]
     outs, st2, handed = gu.gpu_decompress_lat(torch, comps, [len(w) for w in want], dev, group)
-    assert handed == []
-    assert st2 == [0] * len(want)
-    bad = [i for i, (o, w) in enumerate(zip(outs, want)) if o != w]
+    # a node gives up after 64 zero length-extension bytes (runs of ~16 KB and
+    # more: the random and zero blocks of 64 KiB and up), so that a zero run
+    # costs linear time; those blocks go to the exact decoder, and no others
+    long_ext = {i for i, z in enumerate(comps) if bytes(64) in z}
+    assert set(handed) <= long_ext, sorted(set(handed) - long_ext)
+    assert len(handed) <= 6
+    keep = [i for i in range(len(want)) if i not in set(handed)]
+    assert [st2[i] for i in keep] == [0] * len(keep)
+    bad = [i for i in keep if outs[i] != want[i]]
     assert not bad, bad[:8]
 
 
