@@ -266,8 +266,12 @@ def cpu_baseline(plain, comps, seconds, roundtrip=True):
         if c not in counts:
             counts.append(c)
     by = {str(c): measure(c, seconds if c == threads else seconds / 2) for c in counts}
-    top = by[str(threads)]
-    return {"value": top["value"], "unit": "GiB/s", "cores": threads,
+    # the headline is the fastest of them (on a box whose CPU share is smaller
+    # than its affinity set, one thread per CPU oversubscribes the share)
+    best = max(counts, key=lambda c: by[str(c)]["value"])
+    top = by[str(best)]
+    return {"value": top["value"], "unit": "GiB/s", "cores": best,
+            "affinity_cpus": threads,
             "host": host_cpu_info(),
             "kind": kind, "compress_value": top["compress_value"],
             "decompress_value": top["decompress_value"],
@@ -276,9 +280,9 @@ def cpu_baseline(plain, comps, seconds, roundtrip=True):
             "byte_identical_blocks": f"{identical}/{nsample}",
             "sample": f"{nsample} of the same {lens[0]}-byte ITB blocks, round-robin over "
                       f"{threads} threads (one per CPU of the affinity set) for {seconds:.0f} s "
-                      f"(decompress {0.6 * seconds:.0f} s, compress {0.4 * seconds:.0f} s); "
-                      f"by_threads repeats it on {', '.join(str(c) for c in counts[1:])} thread(s) for "
-                      f"{seconds / 2:.0f} s each; "
+                      f"(decompress {0.6 * seconds:.0f} s, compress {0.4 * seconds:.0f} s), "
+                      f"then on {', '.join(str(c) for c in counts[1:])} thread(s) for "
+                      f"{seconds / 2:.0f} s each (by_threads); value and cores: the fastest; "
                       + ("lib/minilzo.c built from the reference sources (oracle/_ref)"
                          if kind == "reference" else "oracle/lzo1x_oracle.c port")}
 
@@ -710,14 +714,24 @@ def run_c5(args, rank):
     try:
         best = None
         for _ in range(max(1, args.steps // 5)):
-            t0 = time.perf_counter()
-            which, err = itb.compress_batch(recs, tmps)         # H2D + kernels + D2H
-            t1 = time.perf_counter()
-            af = itb.AppendFile(path)
+            # the codec alone (H2D + kernels + D2H), then the write path: each
+            # chunk's records appended while the GPU compresses the next chunks
+            # (pom_itb_lzo_compress_append_batch), and the same as two calls
+            tc0 = time.perf_counter()
+            which, err = itb.compress_batch(recs, tmps)
+            tc1 = time.perf_counter()
+            af = itb.AppendFile(path + ".serial")
             outs = [t if w else r for r, t, w in zip(recs, tmps, which)]
-            locs = af.append_batch(outs, [itb.header_fields(o)[0] for o in outs])
+            af.append_batch(outs, [itb.header_fields(o)[0] for o in outs])
+            af.close()
+            tc2 = time.perf_counter()
+            os.unlink(path + ".serial")
+            t0 = time.perf_counter()
+            af = itb.AppendFile(path)
+            which, err, locs = itb.compress_append_batch(recs, tmps, af)
             af.close()
             t2 = time.perf_counter()
+            t1 = t0 + (tc1 - tc0)
             fd = os.open(path, os.O_RDONLY)
             back = itb.read_batch(fd, locs, rbufs)            # pom_itb_read_batch
             os.close(fd)
@@ -733,14 +747,15 @@ def run_c5(args, rank):
                 h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = o[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
                 errors += bytes(h) + bytes(b[itb.ITBH_SIZE: len(o)]) != o
             cur = (t1 - t0, t2 - t0, t4 - t3, t4 - t2, errors, len(comp_idx),
-                   os.path.getsize(path))
+                   os.path.getsize(path), tc2 - tc0)
             if best is None or cur[1] + cur[3] < best[1] + best[3]:
                 best = cur
-        c, w, dcd, r, errors, ncomp, fbytes = best
+        c, w, dcd, r, errors, ncomp, fbytes, wser = best
         xres = _c5_xnet(args, recs, originals, tmps, rbufs, path, itb, xnet, plain_bytes)
         res = {"records": len(recs), "uncompressed_bytes": int(plain_bytes),
                "file_bytes": fbytes, "compressed_records": ncomp,
                "write_gibps": round(plain_bytes / w / GIB, 3),
+               "write_serial_gibps": round(plain_bytes / wser / GIB, 3),
                "read_gibps": round(plain_bytes / r / GIB, 3),
                "compress_pcie_gibps": round(plain_bytes / c / GIB, 3),
                "decompress_pcie_gibps": round(plain_bytes / dcd / GIB, 3),

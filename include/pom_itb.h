@@ -82,6 +82,18 @@ int pom_abuf_append_batch(struct pom_abuf *ab, const void *const *recs, const si
 /* unmaps and trims the file to the appended length */
 int pom_abuf_close(struct pom_abuf *ab);
 
+/* The MDS write-back path on the loopback (mds/txg.c:733-770 compressing,
+ * mdsl/storage.c:455-519 appending): pom_itb_lzo_compress_batch, and every
+ * record oi[b] (h.len bytes) appended to ab as soon as the chunk of the
+ * batch holding it is compressed, while the GPU compresses the next chunks.
+ * locations[b] = the record's file offset (UINT64_MAX for a record with
+ * err[b] == -EINVAL, which is not written).  Records are appended in the
+ * order their chunks finish (largest first), not in index order.  Returns 0,
+ * LZO_E_ERROR when the GPU path is unusable, or the first append's -errno. */
+int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
+                                      uint8_t **oi, int *err, size_t n, struct pom_abuf *ab,
+                                      uint64_t *locations);
+
 /* Reads the ITB record at `location` of fd: the 264-byte header first, then
  * the rest of h.len.  *len = h.len.  -EINVAL: h.len < 264 or > cap. */
 int pom_itb_read(int fd, uint64_t location, uint8_t *buf, size_t cap, size_t *len);

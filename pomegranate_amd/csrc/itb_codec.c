@@ -37,65 +37,170 @@ static uint32_t rd32(const uint8_t *p)
 static void wr32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
 static void wr16(uint8_t *p, uint16_t v) { memcpy(p, &v, 2); }
 
+/* One itb_lzo_compress batch: the arrays of pom_itb_lzo_compress_batch, the
+ * LZO batch's own, and (compress + append) the append file. */
+struct itb_wb {
+    uint8_t *const *in;
+    uint8_t *const *tmp;
+    uint8_t **oi;
+    int *err;
+    const uint8_t **src;
+    uint8_t **dst;
+    uint8_t **aside;        /* when tmp cannot take the worst case */
+    size_t *slen, *dlen;
+    int *st;
+    struct pom_abuf *ab;    /* NULL: compress only */
+    uint64_t *locations;
+    int arc;                /* first append error */
+    pthread_mutex_t mu;     /* (chunks of a multi-GPU batch finish on several threads) */
+};
+
+static void itb_wb_free(struct itb_wb *w, size_t n)
+{
+    if (w->aside)
+        for (size_t b = 0; b < n; b++)
+            free(w->aside[b]);
+    free(w->aside);
+    free(w->src);
+    free(w->dst);
+    free(w->slen);
+    free(w->dlen);
+    free(w->st);
+}
+
+/* mds/itb.c:2904-2921: the payload after the header, into tmp after its header */
+static int itb_wb_init(struct itb_wb *w, uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
+                       uint8_t **oi, int *err, size_t n)
+{
+    memset(w, 0, sizeof(*w));
+    w->in = in;
+    w->tmp = tmp;
+    w->oi = oi;
+    w->err = err;
+    w->src = malloc(n * sizeof(*w->src));
+    w->dst = malloc(n * sizeof(*w->dst));
+    w->aside = calloc(n, sizeof(*w->aside));
+    w->slen = malloc(n * sizeof(*w->slen));
+    w->dlen = malloc(n * sizeof(*w->dlen));
+    w->st = malloc(n * sizeof(*w->st));
+    if (!w->src || !w->dst || !w->aside || !w->slen || !w->dlen || !w->st)
+        return LZO_E_OUT_OF_MEMORY;
+    for (size_t b = 0; b < n; b++) {
+        oi[b] = in[b];
+        const uint32_t len = rd32(in[b] + POM_ITBH_LEN_OFF);
+        w->slen[b] = len >= POM_ITBH_SIZE ? len - POM_ITBH_SIZE : 0;
+        w->src[b] = in[b] + POM_ITBH_SIZE;
+        w->dst[b] = tmp[b] + POM_ITBH_SIZE;
+        const size_t worst = lzo_mi355x_worst_compress(w->slen[b]);
+        if (tmp_cap[b] < POM_ITBH_SIZE + worst) {
+            w->aside[b] = malloc(worst);
+            if (!w->aside[b])
+                return LZO_E_OUT_OF_MEMORY;
+            w->dst[b] = w->aside[b];
+        }
+        err[b] = len >= POM_ITBH_SIZE ? 0 : -EINVAL;
+    }
+    return LZO_E_OK;
+}
+
+/* mds/itb.c:2923-2944 for block b once its compressed bytes are in */
+static void itb_wb_finish(struct itb_wb *w, size_t b)
+{
+    if (w->err[b])
+        return;
+    uint8_t *t = w->tmp[b];
+    memcpy(t, w->in[b], POM_ITBH_SIZE);                        /* the itb header */
+    if (w->st[b] != LZO_E_OK) {
+        w->err[b] = w->st[b];
+        return;
+    }
+    if (w->dlen[b] >= w->slen[b])                              /* impossible to compress */
+        return;
+    if (w->aside[b])
+        memcpy(t + POM_ITBH_SIZE, w->aside[b], w->dlen[b]);
+    wr32(t + POM_ITBH_ZLEN_OFF, rd32(t + POM_ITBH_LEN_OFF));
+    wr32(t + POM_ITBH_LEN_OFF, (uint32_t)(POM_ITBH_SIZE + w->dlen[b]));
+    wr16(t + POM_ITBH_ALGO_OFF, POM_COMPR_LZO);
+    w->oi[b] = t;
+}
+
+/* A chunk of the batch is compressed: finish its records and append them to
+ * the file while the GPU works on the next chunks. */
+static void itb_wb_chunk(void *ctx, const size_t *ids, size_t nb)
+{
+    struct itb_wb *w = ctx;
+    const void **recs = malloc(nb * sizeof(*recs));
+    size_t *lens = malloc(nb * sizeof(*lens));
+    uint64_t *locs = malloc(nb * sizeof(*locs));
+    size_t m = 0;
+    for (size_t i = 0; i < nb; i++) {
+        const size_t b = ids[i];
+        itb_wb_finish(w, b);
+        if (w->ab)
+            w->locations[b] = UINT64_MAX;
+        if (!w->ab || w->err[b] == -EINVAL || !recs || !lens || !locs)
+            continue;
+        recs[m] = w->oi[b];
+        lens[m] = rd32(w->oi[b] + POM_ITBH_LEN_OFF);
+        locs[m] = b;                                           /* (the record's index, for now) */
+        m++;
+    }
+    if (w->ab) {
+        pthread_mutex_lock(&w->mu);
+        int rc = !recs || !lens || !locs ? -ENOMEM : 0;
+        uint64_t *at = rc ? NULL : malloc((m + 1) * sizeof(*at));
+        if (!rc && !at)
+            rc = -ENOMEM;
+        if (!rc && !w->arc)
+            rc = pom_abuf_append_batch(w->ab, recs, lens, m, at);
+        if (!rc)
+            for (size_t i = 0; i < m; i++)
+                w->locations[locs[i]] = at[i];
+        if (rc && !w->arc)
+            w->arc = rc;
+        pthread_mutex_unlock(&w->mu);
+        free(at);
+    }
+    free(recs);
+    free(lens);
+    free(locs);
+}
+
 int pom_itb_lzo_compress_batch(uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
                                uint8_t **oi, int *err, size_t n)
 {
     if (n == 0)
         return LZO_E_OK;
-    const uint8_t **src = malloc(n * sizeof(*src));
-    uint8_t **dst = malloc(n * sizeof(*dst));
-    uint8_t **aside = calloc(n, sizeof(*aside));   /* when tmp cannot take the worst case */
-    size_t *slen = malloc(n * sizeof(*slen));
-    size_t *dlen = malloc(n * sizeof(*dlen));
-    int *st = malloc(n * sizeof(*st));
-    int rc = LZO_E_OUT_OF_MEMORY;
-    if (!src || !dst || !aside || !slen || !dlen || !st)
-        goto out;
-    for (size_t b = 0; b < n; b++) {
-        oi[b] = in[b];
-        const uint32_t len = rd32(in[b] + POM_ITBH_LEN_OFF);
-        slen[b] = len >= POM_ITBH_SIZE ? len - POM_ITBH_SIZE : 0;
-        src[b] = in[b] + POM_ITBH_SIZE;
-        dst[b] = tmp[b] + POM_ITBH_SIZE;
-        const size_t worst = lzo_mi355x_worst_compress(slen[b]);
-        if (tmp_cap[b] < POM_ITBH_SIZE + worst) {
-            aside[b] = malloc(worst);
-            if (!aside[b])
-                goto out;
-            dst[b] = aside[b];
-        }
-        err[b] = len >= POM_ITBH_SIZE ? 0 : -EINVAL;
-    }
-    rc = lzo_mi355x_compress_batch(src, slen, dst, dlen, st, n);
-    if (rc != LZO_E_OK)
-        goto out;
-    for (size_t b = 0; b < n; b++) {
-        if (err[b])
-            continue;
-        memcpy(tmp[b], in[b], POM_ITBH_SIZE);                  /* the itb header */
-        if (st[b] != LZO_E_OK) {
-            err[b] = st[b];
-            continue;
-        }
-        if (dlen[b] >= slen[b])                                /* impossible to compress */
-            continue;
-        if (aside[b])
-            memcpy(tmp[b] + POM_ITBH_SIZE, aside[b], dlen[b]);
-        wr32(tmp[b] + POM_ITBH_ZLEN_OFF, rd32(tmp[b] + POM_ITBH_LEN_OFF));
-        wr32(tmp[b] + POM_ITBH_LEN_OFF, (uint32_t)(POM_ITBH_SIZE + dlen[b]));
-        wr16(tmp[b] + POM_ITBH_ALGO_OFF, POM_COMPR_LZO);
-        oi[b] = tmp[b];
-    }
-out:
-    if (aside)
+    struct itb_wb w;
+    int rc = itb_wb_init(&w, in, tmp, tmp_cap, oi, err, n);
+    if (rc == LZO_E_OK)
+        rc = lzo_mi355x_compress_batch(w.src, w.slen, w.dst, w.dlen, w.st, n);
+    if (rc == LZO_E_OK)
         for (size_t b = 0; b < n; b++)
-            free(aside[b]);
-    free(aside);
-    free(src);
-    free(dst);
-    free(slen);
-    free(dlen);
-    free(st);
+            itb_wb_finish(&w, b);
+    itb_wb_free(&w, n);
+    return rc;
+}
+
+int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
+                                      uint8_t **oi, int *err, size_t n, struct pom_abuf *ab,
+                                      uint64_t *locations)
+{
+    if (n == 0)
+        return LZO_E_OK;
+    if (!ab || !ab->addr || !locations)
+        return -EINVAL;
+    struct itb_wb w;
+    int rc = itb_wb_init(&w, in, tmp, tmp_cap, oi, err, n);
+    w.ab = ab;
+    w.locations = locations;
+    pthread_mutex_init(&w.mu, NULL);
+    if (rc == LZO_E_OK)
+        rc = pom_compress_batch_chunked(w.src, w.slen, w.dst, w.dlen, w.st, n, itb_wb_chunk, &w);
+    if (rc == LZO_E_OK && w.arc)
+        rc = w.arc;
+    pthread_mutex_destroy(&w.mu);
+    itb_wb_free(&w, n);
     return rc;
 }
 

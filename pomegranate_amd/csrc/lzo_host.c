@@ -581,6 +581,8 @@ struct hbatch {
     struct tctx *t;
     uint32_t enc_lds_max;   /* chunks of at most this many blocks: LDS dictionaries */
     int nslots;             /* chunks in flight per device (<= kSlots) */
+    pom_chunk_fn on_chunk;  /* called with each delivered chunk's block ids, or NULL */
+    void *cb_ctx;
 };
 
 /* debug key host_timing=1: per-batch and per-chunk wall times on stderr (diagnostic) */
@@ -860,16 +862,22 @@ static int dev_run(void *arg, int d)
         size_t from = 0;
         for (int k = 0;; k++) {
             const int cur = k % B->nslots, nxt = (k + 1) % B->nslots;
+            const size_t *done_ids = NULL;     /* the chunk delivered now, for on_chunk */
+            size_t done_nb = 0;
             if (live[cur]) {                   /* chunk k - nslots: wait, unpack */
                 if (chunk_deliver(&c->s[cur], &L[cur], B, live[nxt] ? &c->s[nxt] : NULL,
                                   &L[nxt]) != 0) {
                     rc = -1;
                     for (int j = 0; j < B->nslots; j++)
                         hipStreamSynchronize(c->s[j].stream);
+                } else {
+                    done_ids = L[cur].ids;     /* (points into the plan, not the layout) */
+                    done_nb = L[cur].nb;
                 }
                 live[cur] = 0;
             }
-            if (from < nids && rc == 0) {
+            const int more = from < nids && rc == 0;
+            if (more) {
                 const size_t end = pom_chunk_end(ids, from, nids, B->cost,
                                                  k ? B->budget : B->budget / 4, kChunkBlocks);
                 layout_make(&L[cur], ids + from, end - from, B->src_len, B->cap,
@@ -881,7 +889,12 @@ static int dev_run(void *arg, int d)
                     live[cur] = 1;
                 }
                 from = end;
-            } else {
+            }
+            /* the caller's per-chunk work runs while the launched chunks' copies
+             * and kernels are in flight */
+            if (done_ids && B->on_chunk)
+                B->on_chunk(B->cb_ctx, done_ids, done_nb);
+            if (!more) {
                 int any = 0;
                 for (int j = 0; j < B->nslots; j++)
                     any |= live[j];
@@ -921,8 +934,30 @@ static int batch_devices(int *devs)
     return n;
 }
 
+static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
+                           uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks,
+                           pom_chunk_fn on_chunk, void *cb_ctx);
+
 static int batch_common(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
                         uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks)
+{
+    return batch_common_cb(kind, src, src_len, dst, dst_len, status, nblocks, NULL, NULL);
+}
+
+/* lzo_mi355x_compress_batch with on_chunk(ctx, ids, nb) called as each chunk's
+ * blocks (ids into the caller's arrays) are delivered -- from the thread
+ * running that device's chunks, so concurrently for batches split over
+ * several GPUs. */
+int pom_compress_batch_chunked(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                               size_t *dst_len, int *status, size_t nblocks, pom_chunk_fn on_chunk,
+                               void *ctx)
+{
+    return batch_common_cb(OP_COMPRESS, src, src_len, dst, dst_len, status, nblocks, on_chunk, ctx);
+}
+
+static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
+                           uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks,
+                           pom_chunk_fn on_chunk, void *cb_ctx)
 {
     if (g_timing < 0)
         g_timing = pom_dbg_int("host_timing", 0) == 1;
@@ -957,7 +992,7 @@ static int batch_common(enum op_kind kind, const uint8_t *const *src, const size
         cost[b] = src_len[b] + cap[b];
     }
     struct hbatch B = {kind, src, src_len, dst, dst_len, status, cap, cost, kChunkBudget,
-                       {0, 1, NULL, NULL}, devs, t, 0, kSlots};
+                       {0, 1, NULL, NULL}, devs, t, 0, kSlots, on_chunk, cb_ctx};
     /* compress chunks that fit the LDS encoder's 4 blocks per CU at once use
      * it: a block alone on its CU finishes twice as fast as with the
      * dictionaries in HBM (that encoder wins only on full GPUs: 16 per CU) */

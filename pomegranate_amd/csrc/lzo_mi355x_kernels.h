@@ -118,6 +118,15 @@ int lzo_mi355x_launch_decoded_length(const uint8_t *src, const uint64_t *src_off
 const char *pom_dbg_str(const char *key, char *buf, size_t n);
 long pom_dbg_int(const char *key, long dflt);
 
+/* Host side (lzo_host.c), not part of the ABI: lzo_mi355x_compress_batch
+ * with on_chunk(ctx, ids, nb) called as each chunk's blocks are delivered
+ * (ids: indices into the caller's arrays), from the thread running that
+ * device's chunks -- concurrently when the batch is split over GPUs. */
+typedef void (*pom_chunk_fn)(void *ctx, const size_t *ids, size_t nb);
+int pom_compress_batch_chunked(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                               size_t *dst_len, int *status, size_t nblocks, pom_chunk_fn on_chunk,
+                               void *ctx);
+
 /* Host side (lzo_host.c), not part of the ABI: len[i] bytes from src[i] to
  * dst[i] for every i, split over up to 8 threads once the total is large. */
 void pom_copy_parallel(uint8_t *const *dst, const uint8_t *const *src, const size_t *len, size_t n);

@@ -39,6 +39,9 @@ def _lib() -> ctypes.CDLL:
     if not _bound:
         lib.pom_itb_lzo_compress_batch.restype = ctypes.c_int
         lib.pom_itb_lzo_compress_batch.argtypes = [_vp] * 5 + [ctypes.c_size_t]
+        lib.pom_itb_lzo_compress_append_batch.restype = ctypes.c_int
+        lib.pom_itb_lzo_compress_append_batch.argtypes = [_vp] * 5 + [ctypes.c_size_t,
+                                                                      ctypes.POINTER(_Abuf), _vp]
         lib.pom_itb_lzo_decompress_batch.restype = ctypes.c_int
         lib.pom_itb_lzo_decompress_batch.argtypes = [_vp] * 4 + [ctypes.c_size_t]
         lib.pom_abuf_open.restype = ctypes.c_int
@@ -105,6 +108,26 @@ def compress_batch(ins: List[bytearray], tmps: List[bytearray]) -> Tuple[List[in
         raise RuntimeError(f"pom_itb_lzo_compress_batch: {rc}")
     which = [0 if oi[b] == pin[b] else 1 for b in range(n)]
     return which, list(err)
+
+
+def compress_append_batch(ins: List[bytearray], tmps: List[bytearray], af: "AppendFile"):
+    """pom_itb_lzo_compress_append_batch: compresses the records and appends
+    each (compressed or kept) to the append file af as soon as its chunk is
+    done.  Returns (which[b], err[b], location[b]) as compress_batch and
+    AppendFile.append_batch do."""
+    lib = _lib()
+    n = len(ins)
+    pin, k1 = _ptrs(ins)
+    ptmp, k2 = _ptrs(tmps)
+    caps = (ctypes.c_size_t * n)(*[len(t) for t in tmps])
+    oi = (_vp * n)()
+    err = (ctypes.c_int * n)()
+    locs = (ctypes.c_uint64 * max(n, 1))()
+    rc = lib.pom_itb_lzo_compress_append_batch(pin, ptmp, caps, oi, err, n, ctypes.byref(af.ab), locs)
+    if rc != 0:
+        raise RuntimeError(f"pom_itb_lzo_compress_append_batch: {rc}")
+    which = [0 if oi[b] == pin[b] else 1 for b in range(n)]
+    return which, list(err), list(locs[:n])
 
 
 def decompress_batch(ins: List[bytearray]) -> Tuple[List[int], List[int]]:

@@ -48,7 +48,7 @@ EXPORTS = (
     "lzo_mi355x_compress_batch", "lzo_mi355x_decompress_batch",
     "lzo_mi355x_decompress_concat_batch",
     # include/pom_itb.h
-    "pom_itb_lzo_compress_batch", "pom_itb_lzo_decompress_batch",
+    "pom_itb_lzo_compress_batch", "pom_itb_lzo_compress_append_batch", "pom_itb_lzo_decompress_batch",
     "pom_abuf_open", "pom_abuf_append", "pom_abuf_append_batch", "pom_abuf_close", "pom_itb_read",
     "pom_itb_read_batch",
     # include/pom_column.h

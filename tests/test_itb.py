@@ -9,6 +9,7 @@ restores the record byte for byte.
 """
 from __future__ import annotations
 
+import errno
 import os
 import struct
 
@@ -195,6 +196,55 @@ def test_c5_append_file_loop_on_gpu(oracle, tmp_path, win):
     for b, orig in zip(back, originals):
         ln, _, algo = itb.header_fields(b)
         assert algo == itb.COMPR_NONE and ln == len(orig)
+        h = bytearray(b[: itb.ITBH_SIZE])
+        h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = orig[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
+        assert bytes(h) + bytes(b[itb.ITBH_SIZE: ln]) == orig
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk_mb", [0, 1])
+def test_compress_append_batch_on_gpu(oracle, tmp_path, monkeypatch, chunk_mb):
+    """The fused write path (pom_itb_lzo_compress_append_batch): every record
+    is appended as soon as its chunk is compressed (with 1 MiB chunks, many
+    chunks, appended in the order they finish).  Each stored record is the
+    reference's itb_lzo_compress result, the file holds exactly the appended
+    records, a record with h.len below the header is neither compressed nor
+    written (location UINT64_MAX), and every record reads back and decodes to
+    its original."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if chunk_mb:
+        monkeypatch.setenv("POM_LZO_DEBUG", f"chunk_mb={chunk_mb}")
+    recs = _records(60, seed=21) + _records(3, seed=22, model=synth.RANDOM)
+    bad = bytearray(itb.ITB_FULL)
+    struct.pack_into("<I", bad, itb.LEN_OFF, 100)                 # h.len < 264: -EINVAL
+    recs.append(bad)
+    originals = [bytes(r[: itb.header_fields(r)[0]]) for r in recs[:-1]]
+    tmps = [bytearray(itb.ITB_FULL) for _ in recs]
+    path = str(tmp_path / "wb.itb")
+    af = itb.AppendFile(path, win=1 << 20)
+    which, err, locs = itb.compress_append_batch(recs, tmps, af)
+    af.close()
+    assert err[:-1] == [0] * (len(recs) - 1) and err[-1] == -errno.EINVAL
+    assert locs[-1] == (1 << 64) - 1
+    sent = [t if w else r for r, t, w in zip(recs[:-1], tmps, which)]
+    lens = [itb.header_fields(o)[0] for o in sent]
+    assert os.path.getsize(path) == sum(lens)
+    assert sorted(locs[:-1]) == sorted(set(locs[:-1]))
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        back = [itb.read_record(fd, loc) for loc in locs[:-1]]
+    finally:
+        os.close(fd)
+    for b, o, w, orig in zip(back, sent, which, originals):
+        ew, erec = _expected_compress(oracle, bytearray(orig))
+        assert w == ew and bytes(b[: itb.header_fields(b)[0]]) == erec == bytes(o[: len(erec)])
+    comp = [i for i, b in enumerate(back) if itb.header_fields(b)[2] == itb.COMPR_LZO]
+    derr, ok = itb.decompress_batch([back[i] for i in comp])
+    assert derr == [0] * len(comp) and ok == [1] * len(comp)
+    for b, orig in zip(back, originals):
+        ln = itb.header_fields(b)[0]
         h = bytearray(b[: itb.ITBH_SIZE])
         h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = orig[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
         assert bytes(h) + bytes(b[itb.ITBH_SIZE: ln]) == orig
