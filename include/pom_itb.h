@@ -105,6 +105,19 @@ int pom_itb_read(int fd, uint64_t location, uint8_t *buf, size_t cap, size_t *le
 int pom_itb_read_batch(int fd, const uint64_t *locations, size_t n, uint8_t *const *buf,
                        const size_t *cap, size_t *len, int *err);
 
+/* The MDS load path on the loopback (mdsl/storage.c:2507-2640 reading,
+ * mds/itb.c:2949-2980 decoding): pom_itb_read_batch, then, for every record
+ * whose header says COMPR_LZO, pom_itb_lzo_decompress_batch in place -- with
+ * each chunk's payloads read just before the decode batch stages that chunk,
+ * while the GPU decodes the chunks before it.  err[i] = 0 or the read's
+ * -errno (-EINVAL: h.len < 264 or > cap[i]); derr[i] = the decoder's LZO_E_*
+ * code (0 for an uncompressed record); len_ok[i] (may be NULL) as in
+ * pom_itb_lzo_decompress_batch (1 for an uncompressed record); len[i] = the
+ * record's h.len after decoding.  Returns 0, LZO_E_ERROR when the GPU path is
+ * unusable, or LZO_E_OUT_OF_MEMORY. */
+int pom_itb_read_lzo_decompress_batch(int fd, const uint64_t *locations, size_t n, uint8_t *const *buf,
+                                      const size_t *cap, size_t *len, int *err, int *derr, int *len_ok);
+
 #ifdef __cplusplus
 }
 #endif

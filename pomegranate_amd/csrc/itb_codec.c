@@ -498,3 +498,214 @@ int pom_itb_read_batch(int fd, const uint64_t *locations, size_t n, uint8_t *con
     }
     return 0;
 }
+
+
+/* ---- the MDS load path on the loopback: read, then decode as chunks fill ---- */
+struct rd_payload {
+    int fd;
+    const uint64_t *loc;
+    uint8_t *const *buf;
+    const size_t *plen;     /* payload bytes to read per record */
+    int *err;
+    const size_t *ids;      /* records of this job */
+    size_t lo, hi;
+};
+
+static void *payload_worker(void *arg)
+{
+    const struct rd_payload *r = arg;
+    for (size_t i = r->lo; i < r->hi; i++) {
+        const size_t b = r->ids ? r->ids[i] : i;
+        if (r->err[b] || r->plen[b] == 0)
+            continue;
+        r->err[b] = pread_full(r->fd, r->buf[b] + POM_ITBH_SIZE, r->plen[b], r->loc[b] + POM_ITBH_SIZE);
+    }
+    return NULL;
+}
+
+struct rd_header {
+    int fd;
+    const uint64_t *loc;
+    uint8_t *const *buf;
+    int *err;
+    size_t lo, hi;
+};
+
+static void *header_worker(void *arg)
+{
+    const struct rd_header *r = arg;
+    for (size_t b = r->lo; b < r->hi; b++)
+        if (!r->err[b])
+            r->err[b] = pread_full(r->fd, r->buf[b], POM_ITBH_SIZE, r->loc[b]);
+    return NULL;
+}
+
+static void read_headers(int fd, const uint64_t *loc, uint8_t *const *buf, int *err, size_t n)
+{
+    enum { kReadThreads = 8 };
+    const size_t nt = n >= 256 ? kReadThreads : 1;
+    struct rd_header r[kReadThreads];
+    pthread_t th[kReadThreads];
+    int started[kReadThreads] = {0};
+    for (size_t k = 0; k < nt; k++) {
+        r[k] = (struct rd_header){fd, loc, buf, err, n * k / nt, n * (k + 1) / nt};
+        if (k > 0)
+            started[k] = pthread_create(&th[k], NULL, header_worker, &r[k]) == 0;
+    }
+    header_worker(&r[0]);
+    for (size_t k = 1; k < nt; k++) {
+        if (started[k])
+            pthread_join(th[k], NULL);
+        else
+            header_worker(&r[k]);
+    }
+}
+
+/* payloads of records ids[0..n) (ids NULL: 0..n), on up to 8 threads */
+static void read_payloads(int fd, const uint64_t *loc, uint8_t *const *buf, const size_t *plen, int *err,
+                          const size_t *ids, size_t n)
+{
+    enum { kReadThreads = 8 };
+    size_t bytes = 0;
+    for (size_t i = 0; i < n; i++)
+        bytes += plen[ids ? ids[i] : i];
+    const size_t nt = n >= 8 && bytes >= ((size_t)1 << 20) ? kReadThreads : 1;
+    struct rd_payload r[kReadThreads];
+    pthread_t th[kReadThreads];
+    int started[kReadThreads] = {0};
+    for (size_t k = 0; k < nt; k++) {
+        r[k] = (struct rd_payload){fd, loc, buf, plen, err, ids, n * k / nt, n * (k + 1) / nt};
+        if (k > 0)
+            started[k] = pthread_create(&th[k], NULL, payload_worker, &r[k]) == 0;
+    }
+    payload_worker(&r[0]);
+    for (size_t k = 1; k < nt; k++) {
+        if (started[k])
+            pthread_join(th[k], NULL);
+        else
+            payload_worker(&r[k]);
+    }
+}
+
+struct rd_dec {
+    int fd;
+    const uint64_t *loc;    /* per record */
+    uint8_t *const *buf;    /* per record */
+    const size_t *plen;     /* per record */
+    int *err;               /* per record */
+    const size_t *comp;     /* batch block -> record */
+    size_t *tmp_ids;        /* scratch for a chunk's records */
+    pthread_mutex_t mu;     /* (chunks of a multi-GPU batch on several threads) */
+};
+
+/* a chunk of the decode batch is about to be staged: read its payloads */
+static void rd_dec_chunk(void *ctx, const size_t *ids, size_t nb)
+{
+    struct rd_dec *d = ctx;
+    size_t *rec = malloc(nb * sizeof(*rec));
+    if (!rec) {
+        pthread_mutex_lock(&d->mu);
+        for (size_t i = 0; i < nb; i++)
+            d->err[d->comp[ids[i]]] = -ENOMEM;
+        pthread_mutex_unlock(&d->mu);
+        return;
+    }
+    for (size_t i = 0; i < nb; i++)
+        rec[i] = d->comp[ids[i]];
+    read_payloads(d->fd, d->loc, d->buf, d->plen, d->err, rec, nb);
+    free(rec);
+}
+
+int pom_itb_read_lzo_decompress_batch(int fd, const uint64_t *locations, size_t n, uint8_t *const *buf,
+                                      const size_t *cap, size_t *len, int *err, int *derr, int *len_ok)
+{
+    if (n == 0)
+        return LZO_E_OK;
+    size_t *plen = calloc(n, sizeof(*plen));
+    size_t *comp = malloc(n * sizeof(*comp));
+    size_t *unc = malloc(n * sizeof(*unc));
+    const uint8_t **src = malloc(n * sizeof(*src));
+    uint8_t **dst = malloc(n * sizeof(*dst));
+    size_t *slen = malloc(n * sizeof(*slen));
+    size_t *dlen = malloc(n * sizeof(*dlen));
+    int *st = malloc(n * sizeof(*st));
+    int rc = LZO_E_OUT_OF_MEMORY;
+    if (!plen || !comp || !unc || !src || !dst || !slen || !dlen || !st)
+        goto out;
+    /* 1. the headers (mdsl/storage.c:2507-2640 reads the itbh first), on up
+     * to 8 threads */
+    for (size_t b = 0; b < n; b++)
+        err[b] = cap[b] < POM_ITBH_SIZE ? -EINVAL : 0;
+    read_headers(fd, locations, buf, err, n);
+    size_t nc = 0;
+    for (size_t b = 0; b < n; b++) {
+        derr[b] = 0;
+        if (len_ok)
+            len_ok[b] = 0;
+        len[b] = 0;
+        if (err[b])
+            continue;
+        const uint32_t hl = rd32(buf[b] + POM_ITBH_LEN_OFF);
+        if (hl < POM_ITBH_SIZE || hl > cap[b]) {
+            err[b] = -EINVAL;
+            continue;
+        }
+        len[b] = hl;
+        plen[b] = hl - POM_ITBH_SIZE;
+        uint16_t algo;
+        memcpy(&algo, buf[b] + POM_ITBH_ALGO_OFF, 2);
+        if (algo == POM_COMPR_LZO) {
+            comp[nc] = b;
+            src[nc] = buf[b] + POM_ITBH_SIZE;
+            dst[nc] = buf[b] + POM_ITBH_SIZE;       /* in place: staged before written */
+            slen[nc] = plen[b];
+            dlen[nc] = cap[b] - POM_ITBH_SIZE;
+            nc++;
+        } else if (len_ok) {
+            len_ok[b] = 1;
+        }
+    }
+    /* 2. the uncompressed records' payloads; the compressed ones are read chunk
+     * by chunk just before the decode batch stages them */
+    {
+        size_t nu = 0;
+        for (size_t b = 0; b < n; b++) {
+            uint16_t algo;
+            memcpy(&algo, buf[b] + POM_ITBH_ALGO_OFF, 2);
+            if (!err[b] && algo != POM_COMPR_LZO)
+                unc[nu++] = b;
+        }
+        read_payloads(fd, locations, buf, plen, err, unc, nu);
+    }
+    rc = LZO_E_OK;
+    if (nc) {
+        struct rd_dec d = {fd, locations, buf, plen, err, comp, NULL, PTHREAD_MUTEX_INITIALIZER};
+        rc = pom_decompress_batch_chunked(src, slen, dst, dlen, st, nc, rd_dec_chunk, &d);
+        pthread_mutex_destroy(&d.mu);
+    }
+    if (rc != LZO_E_OK)
+        goto out;
+    /* 3. itb_lzo_decompress's header updates (mds/itb.c:2949-2980) */
+    for (size_t i = 0; i < nc; i++) {
+        const size_t b = comp[i];
+        if (err[b])                                 /* (the payload read failed) */
+            continue;
+        const uint32_t zlen = rd32(buf[b] + POM_ITBH_ZLEN_OFF);
+        derr[b] = st[i];
+        if (len_ok)
+            len_ok[b] = st[i] == LZO_E_OK && dlen[i] + POM_ITBH_SIZE == zlen;
+        wr16(buf[b] + POM_ITBH_ALGO_OFF, POM_COMPR_NONE);
+        wr32(buf[b] + POM_ITBH_LEN_OFF, (uint32_t)(dlen[i] + POM_ITBH_SIZE));
+        len[b] = dlen[i] + POM_ITBH_SIZE;
+    }
+out:
+    free(plen);
+    free(comp);
+    free(unc);
+    free(src);
+    free(dst);
+    free(slen);
+    free(dlen);
+    free(st);
+    return rc;
+}

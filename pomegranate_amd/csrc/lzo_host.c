@@ -582,6 +582,7 @@ struct hbatch {
     uint32_t enc_lds_max;   /* chunks of at most this many blocks: LDS dictionaries */
     int nslots;             /* chunks in flight per device (<= kSlots) */
     pom_chunk_fn on_chunk;  /* called with each delivered chunk's block ids, or NULL */
+    pom_chunk_fn pre_chunk; /* called with a chunk's block ids before its inputs are staged */
     void *cb_ctx;
 };
 
@@ -882,6 +883,10 @@ static int dev_run(void *arg, int d)
                                                  k ? B->budget : B->budget / 4, kChunkBlocks);
                 layout_make(&L[cur], ids + from, end - from, B->src_len, B->cap,
                             B->kind == OP_COMPRESS);
+                /* the caller may produce the chunk's inputs now (e.g. read them),
+                 * while the chunks in flight are copied and decoded */
+                if (B->pre_chunk)
+                    B->pre_chunk(B->cb_ctx, ids + from, end - from);
                 if (chunk_launch(&c->s[cur], &L[cur], B) != 0) {
                     rc = -1;
                     hipStreamSynchronize(c->s[cur].stream);
@@ -936,12 +941,23 @@ static int batch_devices(int *devs)
 
 static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
                            uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks,
-                           pom_chunk_fn on_chunk, void *cb_ctx);
+                           pom_chunk_fn on_chunk, pom_chunk_fn pre_chunk, void *cb_ctx);
 
 static int batch_common(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
                         uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks)
 {
-    return batch_common_cb(kind, src, src_len, dst, dst_len, status, nblocks, NULL, NULL);
+    return batch_common_cb(kind, src, src_len, dst, dst_len, status, nblocks, NULL, NULL, NULL);
+}
+
+/* lzo_mi355x_decompress_batch with pre_chunk(ctx, ids, nb) called before each
+ * chunk's inputs are staged: the caller fills src[ids[i]] (src_len is known
+ * up front) while earlier chunks are on the GPU.  Same threads as
+ * pom_compress_batch_chunked. */
+int pom_decompress_batch_chunked(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                                 size_t *dst_len, int *status, size_t nblocks, pom_chunk_fn pre_chunk,
+                                 void *ctx)
+{
+    return batch_common_cb(OP_DECOMPRESS, src, src_len, dst, dst_len, status, nblocks, NULL, pre_chunk, ctx);
 }
 
 /* lzo_mi355x_compress_batch with on_chunk(ctx, ids, nb) called as each chunk's
@@ -952,12 +968,12 @@ int pom_compress_batch_chunked(const uint8_t *const *src, const size_t *src_len,
                                size_t *dst_len, int *status, size_t nblocks, pom_chunk_fn on_chunk,
                                void *ctx)
 {
-    return batch_common_cb(OP_COMPRESS, src, src_len, dst, dst_len, status, nblocks, on_chunk, ctx);
+    return batch_common_cb(OP_COMPRESS, src, src_len, dst, dst_len, status, nblocks, on_chunk, NULL, ctx);
 }
 
 static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const size_t *src_len,
                            uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks,
-                           pom_chunk_fn on_chunk, void *cb_ctx)
+                           pom_chunk_fn on_chunk, pom_chunk_fn pre_chunk, void *cb_ctx)
 {
     if (g_timing < 0)
         g_timing = pom_dbg_int("host_timing", 0) == 1;
@@ -992,7 +1008,7 @@ static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const s
         cost[b] = src_len[b] + cap[b];
     }
     struct hbatch B = {kind, src, src_len, dst, dst_len, status, cap, cost, kChunkBudget,
-                       {0, 1, NULL, NULL}, devs, t, 0, kSlots, on_chunk, cb_ctx};
+                       {0, 1, NULL, NULL}, devs, t, 0, kSlots, on_chunk, pre_chunk, cb_ctx};
     /* compress chunks that fit the LDS encoder's 4 blocks per CU at once use
      * it: a block alone on its CU finishes twice as fast as with the
      * dictionaries in HBM (that encoder wins only on full GPUs: 16 per CU) */

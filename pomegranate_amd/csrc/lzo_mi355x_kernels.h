@@ -126,6 +126,11 @@ typedef void (*pom_chunk_fn)(void *ctx, const size_t *ids, size_t nb);
 int pom_compress_batch_chunked(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
                                size_t *dst_len, int *status, size_t nblocks, pom_chunk_fn on_chunk,
                                void *ctx);
+/* lzo_mi355x_decompress_batch with pre_chunk(ctx, ids, nb) called before each
+ * chunk's inputs are staged (the caller fills src[ids[i]] then). */
+int pom_decompress_batch_chunked(const uint8_t *const *src, const size_t *src_len, uint8_t *const *dst,
+                                 size_t *dst_len, int *status, size_t nblocks, pom_chunk_fn pre_chunk,
+                                 void *ctx);
 
 /* Host side (lzo_host.c), not part of the ABI: len[i] bytes from src[i] to
  * dst[i] for every i, split over up to 8 threads once the total is large. */

@@ -56,6 +56,8 @@ def _lib() -> ctypes.CDLL:
         lib.pom_itb_read.restype = ctypes.c_int
         lib.pom_itb_read.argtypes = [ctypes.c_int, ctypes.c_uint64, _vp, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_size_t)]
+        lib.pom_itb_read_lzo_decompress_batch.restype = ctypes.c_int
+        lib.pom_itb_read_lzo_decompress_batch.argtypes = [ctypes.c_int, _vp, ctypes.c_size_t] + [_vp] * 6
         lib.pom_itb_read_batch.restype = ctypes.c_int
         lib.pom_itb_read_batch.argtypes = [ctypes.c_int, _vp, ctypes.c_size_t, _vp, _vp, _vp, _vp]
         _bound = True
@@ -237,3 +239,23 @@ def read_record(fd: int, location: int, cap: int = ITB_FULL,
     if rc:
         raise OSError(-rc, os.strerror(-rc))
     return buf
+
+
+def read_decompress_batch(fd: int, locations, outs):
+    """pom_itb_read_lzo_decompress_batch: record i at locations[i] into outs[i]
+    (writable buffers, len = cap), LZO records decoded in place as their
+    chunks are read.  Returns (outs, err, derr, len_ok)."""
+    lib = _lib()
+    n = len(locations)
+    loc = (ctypes.c_uint64 * max(n, 1))(*locations)
+    pbuf, keep = _ptrs(outs)
+    caps = (ctypes.c_size_t * max(n, 1))(*[len(o) for o in outs])
+    lens = (ctypes.c_size_t * max(n, 1))()
+    err = (ctypes.c_int * max(n, 1))()
+    derr = (ctypes.c_int * max(n, 1))()
+    ok = (ctypes.c_int * max(n, 1))()
+    rc = lib.pom_itb_read_lzo_decompress_batch(fd, loc, n, pbuf, caps, lens, err, derr, ok)
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"pom_itb_read_lzo_decompress_batch: {rc}")
+    return outs, list(err[:n]), list(derr[:n]), list(ok[:n])

@@ -50,7 +50,7 @@ EXPORTS = (
     # include/pom_itb.h
     "pom_itb_lzo_compress_batch", "pom_itb_lzo_compress_append_batch", "pom_itb_lzo_decompress_batch",
     "pom_abuf_open", "pom_abuf_append", "pom_abuf_append_batch", "pom_abuf_close", "pom_itb_read",
-    "pom_itb_read_batch",
+    "pom_itb_read_batch", "pom_itb_read_lzo_decompress_batch",
     # include/pom_column.h
     "pom_col_zip_bound", "pom_col_zip_batch", "pom_col_zipv", "pom_col_unzip_batch",
     # include/pom_xnet.h

@@ -9,7 +9,7 @@ TAG=${1:?tag}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-python -c "import __graft_entry__ as g; g.build()" > $OUT/build.log 2>&1 || exit 1
+# (the library is built in-tree before the call: it travels with the snapshot)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-others > $OUT/bench_traced.log 2>&1 || { echo trace failed; tail $OUT/bench_traced.log; exit 1; }
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_INST_ANY"
 for op in decode encode; do

@@ -203,14 +203,15 @@ def test_c5_append_file_loop_on_gpu(oracle, tmp_path, win):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("chunk_mb", [0, 1])
-def test_compress_append_batch_on_gpu(oracle, tmp_path, monkeypatch, chunk_mb):
+def test_compress_append_and_read_decompress_on_gpu(oracle, tmp_path, monkeypatch, chunk_mb):
     """The fused write path (pom_itb_lzo_compress_append_batch): every record
     is appended as soon as its chunk is compressed (with 1 MiB chunks, many
     chunks, appended in the order they finish).  Each stored record is the
     reference's itb_lzo_compress result, the file holds exactly the appended
     records, a record with h.len below the header is neither compressed nor
     written (location UINT64_MAX), and every record reads back and decodes to
-    its original."""
+    its original -- through the two-call load path and through the fused one
+    (pom_itb_read_lzo_decompress_batch)."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -245,6 +246,21 @@ def test_compress_append_batch_on_gpu(oracle, tmp_path, monkeypatch, chunk_mb):
     assert derr == [0] * len(comp) and ok == [1] * len(comp)
     for b, orig in zip(back, originals):
         ln = itb.header_fields(b)[0]
+        h = bytearray(b[: itb.ITBH_SIZE])
+        h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = orig[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
+        assert bytes(h) + bytes(b[itb.ITBH_SIZE: ln]) == orig
+    # the load path fused the same way (pom_itb_read_lzo_decompress_batch):
+    # payloads read chunk by chunk just before the decode batch stages them
+    outs = [bytearray(itb.ITB_FULL) for _ in originals]
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        outs, rerr, derr2, ok2 = itb.read_decompress_batch(fd, locs[:-1], outs)
+    finally:
+        os.close(fd)
+    assert rerr == [0] * len(outs) and derr2 == [0] * len(outs) and ok2 == [1] * len(outs)
+    for b, orig in zip(outs, originals):
+        ln, _, algo = itb.header_fields(b)
+        assert algo == itb.COMPR_NONE and ln == len(orig)
         h = bytearray(b[: itb.ITBH_SIZE])
         h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = orig[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
         assert bytes(h) + bytes(b[itb.ITBH_SIZE: ln]) == orig
