@@ -854,6 +854,8 @@ def run_single(args, lzo, synth):
                     back.raw[:n] == d
         return ok
 
+    z0, zl0 = ctypes.create_string_buffer(n + n // 16 + 128), ulong(0)
+    lib.lzo1x_1_compress(bufs[0][0], n, z0, ctypes.byref(zl0), None)
     conc = {"threads": nthr, "calls_per_thread": per, "block_bytes": n}
     for what in ("compress", "decompress"):
         with ThreadPoolExecutor(nthr) as ex:            # (untimed: staging grows to its groups)
@@ -865,6 +867,16 @@ def run_single(args, lzo, synth):
         errors += oks.count(False)
         conc[f"{what}_calls_per_s"] = round(nthr * per / dt, 1)
         conc[f"{what}_serial_calls_per_s"] = round(1e6 / out["65536"]["gpu"][f"{what}_us"], 1)
+        # a lone call right after the group: the library's leader waits up to
+        # ~50 us for company when the last group had some
+        src, z, back = bufs[0]
+        zl, ol = ulong(0), ulong(0)
+        t0 = time.perf_counter()
+        if what == "compress":
+            errors += lib.lzo1x_1_compress(src, n, z, ctypes.byref(zl), None) != 0
+        else:
+            errors += lib.lzo1x_decompress(z0, zl0.value, back, ctypes.byref(ol), None) != 0
+        conc[f"{what}_lone_after_group_us"] = round((time.perf_counter() - t0) * 1e6, 1)
     result = {
         "metric": "LZO1X single-call latency, lzo1x_decompress of one 64 KiB ITB block (us)",
         "value": v, "unit": "us", "n_gpus": 1, "steps": max(3, args.steps), "warmup": 1,
