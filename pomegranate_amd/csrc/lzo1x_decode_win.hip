@@ -149,7 +149,21 @@ __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t po
     bool capped = false;
     auto ext = [&](uint32_t& p, uint32_t base) -> uint32_t {
         uint32_t v = 0;
-        while (p < k.z && rd(p) == 0) {
+        while (p < k.z) {
+            // (past the staged piece, aligned 16-byte reads take a long zero
+            // run 16 bytes at a time: such a read never leaves the page of the
+            // block's byte at p)
+            if (!spec && p >= k.sEnd && p + 16 <= k.z && ((uintptr_t)(k.in + p) & 15u) == 0) {
+                const uint4 w = *(const uint4*)(k.in + p);
+                if ((w.x | w.y | w.z | w.w) == 0) {
+                    v += 255u * 16;
+                    p += 16;
+                    far = p > far ? p : far;
+                    continue;
+                }
+            }
+            if (rd(p) != 0)
+                break;
             v += 255;
             p++;
             if (spec && v > 255u * kMaxExtZeros) {

@@ -1121,6 +1121,7 @@ struct sc_req {
     size_t produced;
     int rc;
     int done;
+    uint64_t group;             /* sequence number of the group that ran it */
     struct sc_req *next;
 };
 
@@ -1130,11 +1131,13 @@ struct sc_queue {
     struct sc_req *head, *tail;
     int leader;
     int last_k;                 /* size of the last group (a hint that callers come together) */
+    uint64_t seq;               /* groups run so far */
     int ready;                  /* slot and stream below created */
     struct slot slot;           /* the groups' staging: one leader at a time per device */
 };
 
 static struct sc_queue sc_q[kMaxDev];
+static __thread uint64_t sc_last_group;      /* group of this thread's last single call */
 static pthread_once_t sc_once = PTHREAD_ONCE_INIT;
 
 static void sc_init(void)
@@ -1374,7 +1377,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
     if (src_len > 0xFFFFFFF0u || room > 0xFFFFFFF0u || lzo_mi355x_device_count() <= 0 ||
         hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev)
         return LZO_E_ERROR;
-    struct sc_req r = {kind, src, src_len, dst, room, 0, LZO_E_ERROR, 0, NULL};
+    struct sc_req r = {kind, src, src_len, dst, room, 0, LZO_E_ERROR, 0, 0, NULL};
     if (!sc_combine()) {
         struct sc_req *g = &r;
         sc_run_group(&g, 1, NULL);
@@ -1396,11 +1399,13 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
             pthread_cond_wait(&q->cv, &q->mu);
             continue;
         }
-        /* lead: the queue's oldest calls of the oldest call's kind.  When the
-         * last group had company and this one would not, the other callers
-         * are probably between two calls: give them ~50 us to queue */
+        /* lead: the queue's oldest calls of the oldest call's kind.  When this
+         * thread's previous call was in the last group and that group had
+         * company, the other callers are probably between two calls: give
+         * them ~50 us to queue.  (A thread that was not in it -- a lone caller
+         * after a burst of others -- does not wait: ADVICE round 3.) */
         q->leader = 1;
-        if (q->last_k > 1 && q->head == q->tail) {
+        if (q->last_k > 1 && q->head == q->tail && sc_last_group == q->seq) {
             struct timespec ts;
             clock_gettime(CLOCK_MONOTONIC, &ts);
             ts.tv_nsec += 50000;
@@ -1433,13 +1438,17 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
         pthread_mutex_unlock(&q->mu);
         sc_run_group(g, k, q);
         pthread_mutex_lock(&q->mu);
-        for (int i = 0; i < k; i++)
+        q->seq++;
+        for (int i = 0; i < k; i++) {
             g[i]->done = 1;
+            g[i]->group = q->seq;
+        }
         q->leader = 0;
         q->last_k = k;
         pthread_cond_broadcast(&q->cv);
     }
     pthread_mutex_unlock(&q->mu);
+    sc_last_group = r.group;
     *produced = r.produced;
     return r.rc;
 }
