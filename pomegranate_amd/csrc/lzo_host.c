@@ -838,6 +838,12 @@ static int chunk_deliver(struct slot *S, struct layout *L, const struct hbatch *
  * long serial LZ chains start while the rest of the batch is still being
  * copied up.  Debug key chunk_mb overrides the budget. */
 static const size_t kChunkBudget = (size_t)128 << 20;
+/* compress batches take twice that: their chains are long (a 536 KB ITB is
+ * ~6 ms on one CU), so fewer, larger chunks all get in flight at once -- C5's
+ * 1,024 records compress at 17.5 against 14.5 GiB/s (PCIe included) with 256
+ * against 128 MiB; decode batches are faster with 128 (25.2 against 23.0 GiB/s
+ * read), where the copies are the larger share (profiles/r04b) */
+static const size_t kChunkBudgetCompress = (size_t)256 << 20;
 static const size_t kChunkBlocks = (size_t)1 << 20;
 /* below this many bytes per device a batch stays on one device */
 static const size_t kSplitMinBytes = (size_t)64 << 20;
@@ -1007,7 +1013,8 @@ static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const s
             cap[b] = 0xFFFFFFF0u;
         cost[b] = src_len[b] + cap[b];
     }
-    struct hbatch B = {kind, src, src_len, dst, dst_len, status, cap, cost, kChunkBudget,
+    struct hbatch B = {kind, src, src_len, dst, dst_len, status, cap, cost,
+                       kind == OP_COMPRESS ? kChunkBudgetCompress : kChunkBudget,
                        {0, 1, NULL, NULL}, devs, t, 0, kSlots, on_chunk, pre_chunk, cb_ctx};
     /* compress chunks that fit the LDS encoder's 4 blocks per CU at once use
      * it: a block alone on its CU finishes twice as fast as with the
