@@ -64,9 +64,6 @@ constexpr uint32_t kFarPos = 0xC0000000u;        // a read position past every b
 #ifndef POM_EMIT_SLEEP
 #define POM_EMIT_SLEEP 8
 #endif
-#ifndef POM_ENC_NOZERO
-#define POM_ENC_NOZERO 0                         // counterfactual A/B build only: output NOT valid
-#endif
 #ifndef POM_ENC_AHEAD
 #define POM_ENC_AHEAD 2048                      // bytes the emit wave pulls into L2 ahead of the parse
 #endif
@@ -549,7 +546,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
     const BlockSrc B = block_src(in, n);
     uint32_t ii = 0;                                // first byte not yet emitted
     if (n > 13) {                                   // lib/minilzo.c:3167-3173
-        for (uint32_t s = l; s < (GD && POM_ENC_NOZERO ? 0u : kSlots / 2); s += kWave)
+        for (uint32_t s = l; s < kSlots / 2; s += kWave)
             D.put2(s, 0);                           // zero-filled wrkmem: all EMPTY
         for (uint32_t s = l; s < kClaim; s += kWave)
             S.claim[s] = 0xFFFFFFFFu;               // (tag 0xFFFFFF: no window has it)
@@ -845,354 +842,6 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
 #undef ESTAMP
 }
 
-// ---------------------------------------------------------------------------
-// 128-position windows (one-wave global-dictionary kernel, debug key enc_w2):
-// lane l probes positions ip + l (set 0) and ip + 64 + l (set 1), virtual
-// lane v = 64 * set + l.  The same protocol as parse_wave -- probes against
-// the pre-window dictionary, the greedy path from v = 0, claims and
-// forwarding among path lanes, tokens, UPDATE_I -- over 128 positions, so a
-// block takes ~2/3 of the windows (each window's dictionary-probe and
-// candidate round trips are shared by twice the positions).
-// ---------------------------------------------------------------------------
-#ifndef POM_ENC_PATHMAX2
-#define POM_ENC_PATHMAX2 12                      // matches per 128-position window
-#endif
-struct W2Set {
-    uint32_t pw[kCmpW];                          // probe words at the lane's position
-    uint32_t h1, h2, slot, cand, mlen;
-    bool ok, use2;
-};
-
-__device__ __forceinline__ uint32_t ctz2(const uint64_t (&m)[2], uint32_t from)
-{
-    // first set bit >= from of a 128-bit mask, or 128
-    const uint64_t a = from < 64 ? m[0] & (~0ull << from) : 0ull;
-    if (a)
-        return (uint32_t)__builtin_ctzll(a);
-    const uint64_t b = from < 64 ? m[1] : from < 128 ? m[1] & (~0ull << (from - 64)) : 0ull;
-    return b ? 64u + (uint32_t)__builtin_ctzll(b) : 128u;
-}
-__device__ __forceinline__ uint32_t clz_below2(const uint64_t (&m)[2], uint32_t below)
-{
-    // highest set bit < below, or 0xFFFFFFFF
-    const uint64_t b = below > 64 ? m[1] & (below >= 128 ? ~0ull : ((1ull << (below - 64)) - 1)) : 0ull;
-    if (b)
-        return 127u - (uint32_t)__builtin_clzll(b);
-    const uint64_t a = m[0] & (below >= 64 ? ~0ull : ((1ull << below) - 1));
-    return a ? 63u - (uint32_t)__builtin_clzll(a) : 0xFFFFFFFFu;
-}
-__device__ __forceinline__ void set_range2(uint64_t (&m)[2], uint32_t lo, uint32_t hi)
-{
-    // bits [lo, hi), hi <= 128
-    auto rng = [](uint32_t a, uint32_t b) -> uint64_t {    // bits [a, b) of one word, 0 <= a <= b <= 64
-        if (a >= b)
-            return 0ull;
-        const uint64_t hm = b >= 64 ? ~0ull : ((1ull << b) - 1);
-        return hm & (~0ull << a);
-    };
-    m[0] |= rng(lo < 64 ? lo : 64, hi < 64 ? hi : 64);
-    m[1] |= rng(lo > 64 ? lo - 64 : 0, hi > 64 ? hi - 64 : 0);
-}
-__device__ __forceinline__ void keep_below2(uint64_t (&m)[2], uint32_t c)
-{
-    m[0] &= c >= 64 ? ~0ull : ((1ull << c) - 1);
-    m[1] &= c >= 128 ? ~0ull : c <= 64 ? 0ull : ((1ull << (c - 64)) - 1);
-}
-__device__ __forceinline__ uint32_t popc_below2(const uint64_t (&m)[2], uint32_t v)
-{
-    const uint64_t a = m[0] & (v >= 64 ? ~0ull : ((1ull << v) - 1));
-    const uint64_t b = v <= 64 ? 0ull : m[1] & (v >= 128 ? ~0ull : ((1ull << (v - 64)) - 1));
-    return (uint32_t)__builtin_popcountll(a) + (uint32_t)__builtin_popcountll(b);
-}
-
-__device__ void parse_wave_w2(EncLdsT<true>& S, const Dict<true> D, const uint8_t* in, uint32_t n, uint32_t l,
-                              Emitter<true>* E)
-{
-    uint32_t tp = 0;                                // tokens produced
-    const uintptr_t pf_lines = (uintptr_t)in & ~(uintptr_t)127;
-    const uintptr_t pf_last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
-    uint32_t pf = 0, pf_acc = 0, pf_new = 0;
-    auto prefetch = [&](uint32_t at) {
-        pf_acc ^= pf_new;
-        pf_new = 0;
-        const uint32_t ahead = at + POM_ENC_AHEAD;
-        const uint32_t want = ahead < n + 127 ? ahead : n + 127;
-        for (; pf < want; pf += 128 * kWave) {
-            const uintptr_t a = pf_lines + pf + 128 * l;
-            if (a <= pf_last)
-                pf_new ^= *(gdword*)a;
-        }
-    };
-    const BlockSrc B = block_src(in, n);
-    uint32_t ii = 0;                                // first byte not yet emitted
-    if (n > 13) {                                   // lib/minilzo.c:3167-3173
-        for (uint32_t s2 = l; s2 < (POM_ENC_NOZERO ? 0u : kSlots / 2); s2 += kWave)
-            D.put2(s2, 0);                          // zero-filled wrkmem: all EMPTY
-        for (uint32_t s2 = l; s2 < kClaim; s2 += kWave)
-            S.claim[s2] = 0xFFFFFFFFu;
-        __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0): the table is zero in L2
-        wave_order();
-        const uint32_t ip_end = n - 13;             // lib/minilzo.c:2929
-        uint32_t ip = 4;
-        uint32_t base = 0;
-        uint32_t wtag = 0xFFFFFEu;
-        W2Set X[2];
-        load_at<kCmpW>(B, ip + l, X[0].pw);
-        load_at<kCmpW>(B, ip + kWave + l, X[1].pw);
-        for (;;) {
-#if POM_ENC_PRIO
-            if (E->prio) {
-                const uint32_t left = n - ip, st = POM_ENC_PRIO_STEP;
-                const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
-                                                                  : left >= st ? 1u : 0u);
-                switch (q) {
-                case 3: __builtin_amdgcn_s_setprio(3); break;
-                case 2: __builtin_amdgcn_s_setprio(2); break;
-                case 1: __builtin_amdgcn_s_setprio(1); break;
-                default: __builtin_amdgcn_s_setprio(0); break;
-                }
-            }
-#endif
-            if (ip + 2 * kWave - base >= 0xFFFFu) { // this window's positions would not fit
-                const uint32_t nb = (ip - (kM4MaxOffset + 1)) / kRebase * kRebase;
-                const uint32_t delta = nb - base;
-                for (uint32_t s2 = l; s2 < kSlots / 2; s2 += kWave) {
-                    const uint32_t pr = D.get2(s2);
-                    const uint32_t lo = pr & 0xFFFFu, hi = pr >> 16;
-                    const uint32_t nlo = lo > delta ? lo - delta : 0u;
-                    const uint32_t nhi = hi > delta ? hi - delta : 0u;
-                    D.put2(s2, nlo | (nhi << 16));
-                }
-                __builtin_amdgcn_s_waitcnt(0x0F70);
-                wave_order();
-                base = nb;
-            }
-            if (POM_ENC_AHEAD)
-                prefetch(ip);
-            uint32_t p[2];
-            bool active[2];
-            uint64_t am[2];
-            uint32_t w1[2], w2[2];
-            bool v1[2], v2[2];
-#pragma unroll
-            for (int st = 0; st < 2; st++) {
-                p[st] = ip + kWave * st + l;
-                active[st] = (st == 0 && l == 0) || p[st] < ip_end;
-                am[st] = mask_lt(p[st], ip_end) | (st == 0 ? 1ull : 0ull);
-                X[st].h1 = emit::slot_primary(X[st].pw[0] & 0xFF, (X[st].pw[0] >> 8) & 0xFF,
-                                              (X[st].pw[0] >> 16) & 0xFF, X[st].pw[0] >> 24);
-                X[st].h2 = emit::slot_secondary(X[st].h1);
-            }
-            uint32_t e1[2], e2[2];
-#pragma unroll
-            for (int st = 0; st < 2; st++) {
-                e1[st] = D.get(X[st].h1);
-                e2[st] = D.get(X[st].h2);
-            }
-            const uint32_t nact = (uint32_t)__builtin_popcountll(am[0]) + (uint32_t)__builtin_popcountll(am[1]);
-            uint32_t c1w[2][kCmpW], c2w[2][kCmpW];
-#pragma unroll
-            for (int st = 0; st < 2; st++) {
-                w1[st] = active[st] && e1[st] ? base + e1[st] - 1 : 0u;
-                w2[st] = active[st] && e2[st] ? base + e2[st] - 1 : 0u;
-                v1[st] = active[st] && w1[st] != 0 && p[st] - w1[st] <= kM4MaxOffset;
-                v2[st] = v1[st] && w2[st] != 0 && p[st] - w2[st] <= kM4MaxOffset;
-                load_at<kCmpW, POM_CAND_AUX>(B, v1[st] ? w1[st] : kFarPos, c1w[st]);
-                load_at<kCmpW, POM_CAND_AUX>(B, v2[st] && p[st] - w1[st] > kM2MaxOffset ? w2[st] : kFarPos, c2w[st]);
-            }
-            uint64_t okm[2], um2[2];
-#pragma unroll
-            for (int st = 0; st < 2; st++) {
-                const uint32_t b3 = X[st].pw[0] >> 24;
-                const bool c1pass = v1[st] && (p[st] - w1[st] <= kM2MaxOffset || (c1w[st][0] >> 24) == b3);
-                X[st].use2 = v1[st] && !c1pass;
-                const bool c2pass = X[st].use2 && v2[st] && (p[st] - w2[st] <= kM2MaxOffset || (c2w[st][0] >> 24) == b3);
-                const bool tm = c1pass || c2pass;
-                X[st].slot = X[st].use2 ? X[st].h2 : X[st].h1;
-                X[st].cand = c2pass ? w2[st] : w1[st];
-                uint32_t cw[kCmpW];
-#pragma unroll
-                for (int i = 0; i < kCmpW; i++)
-                    cw[i] = c2pass ? c2w[st][i] : c1w[st][i];
-                X[st].ok = tm && ((cw[0] ^ X[st].pw[0]) & 0xFFFFFFu) == 0;
-                uint32_t ml = first_diff<kCmpW>(cw, X[st].pw);
-                X[st].mlen = ml < n - p[st] ? ml : n - p[st];
-                okm[st] = wave_ballot(X[st].ok);
-                um2[st] = wave_ballot(X[st].use2);
-            }
-
-            // ---- the greedy path over the 128 positions --------------------
-            uint64_t path[2] = {0, 0}, mstart[2] = {0, 0};
-            uint32_t end = 0, nmatch = 0;
-            auto walk = [&](uint32_t from) {
-                end = from;
-                while (end < nact) {
-                    const uint32_t q = ctz2(okm, end);
-                    const uint32_t lit_end = q < nact ? q : nact;
-                    if (lit_end > end)
-                        set_range2(path, end, lit_end);
-                    if (q >= nact) {
-                        end = nact;
-                        break;
-                    }
-                    path[q >> 6] |= 1ull << (q & 63);
-                    mstart[q >> 6] |= 1ull << (q & 63);
-                    const uint32_t qs = q >> 6, ql = q & 63;
-                    uint32_t len = lane_read(qs ? X[1].mlen : X[0].mlen, ql);
-                    if (len == kCmpB && n - (ip + q) > kCmpB) {
-                        len = extend_match(B, n, lane_read(qs ? X[1].cand : X[0].cand, ql), ip + q, kCmpB, l);
-                        if (qs)
-                            X[1].mlen = l == ql ? len : X[1].mlen;
-                        else
-                            X[0].mlen = l == ql ? len : X[0].mlen;
-                    }
-                    end = q + len;
-                    if (++nmatch >= POM_ENC_PATHMAX2)
-                        break;
-                }
-            };
-            walk(0);
-
-            // ---- claims among the path lanes, and forwarding ---------------
-            uint64_t resolved[2] = {0, 0}, superseded[2] = {0, 0};
-            for (uint32_t round = 0;; round++) {
-                uint64_t cm[2];
-#pragma unroll
-                for (int st = 0; st < 2; st++) {
-                    const bool onpath = (path[st] >> l) & 1ull;
-                    atomicMin(&S.claim[onpath ? claim_index(X[st].slot) : kClaim], (wtag << 8) | (kWave * st + l));
-                }
-                wave_order();
-#pragma unroll
-                for (int st = 0; st < 2; st++) {
-                    const uint32_t v = kWave * st + l;
-                    const uint32_t t1 = S.claim[claim_index(X[st].h1)];
-                    const uint32_t t2 = S.claim[claim_index(X[st].h2)];
-                    const uint64_t cf1 = mask_eq(t1 >> 8, wtag) & mask_lt(t1 & 0xFFu, v);
-                    const uint64_t cf2 = um2[st] & mask_eq(t2 >> 8, wtag) & mask_lt(t2 & 0xFFu, v);
-                    cm[st] = path[st] & ~resolved[st] & (cf1 | cf2);
-                }
-                wtag--;
-                if (!cm[0] && !cm[1])
-                    break;
-                const uint32_t c = cm[0] ? (uint32_t)__builtin_ctzll(cm[0]) : 64u + (uint32_t)__builtin_ctzll(cm[1]);
-                if (round >= POM_ENC_FWD) {
-                    end = c;                         // the window ends at a path lane
-                    break;
-                }
-                const uint32_t cs = c >> 6, cl = c & 63;
-                resolved[cs] |= 1ull << cl;
-                uint64_t pm[2] = {path[0], path[1]};
-                keep_below2(pm, c);                  // exact path lanes below c
-                const uint32_t h1c = lane_read(cs ? X[1].h1 : X[0].h1, cl);
-                const uint32_t h2c = lane_read(cs ? X[1].h2 : X[0].h2, cl);
-                const bool c2 = (um2[cs] >> cl) & 1ull;
-                uint64_t wm1[2], wm2[2];
-#pragma unroll
-                for (int st = 0; st < 2; st++) {
-                    wm1[st] = wave_ballot(X[st].slot == h1c) & pm[st];
-                    wm2[st] = c2 ? wave_ballot(X[st].slot == h2c) & pm[st] : 0ull;
-                }
-                if (!wm1[0] && !wm1[1] && !wm2[0] && !wm2[1])
-                    continue;                        // a claim-table alias: c was exact
-                const bool via2 = !wm1[0] && !wm1[1];
-                const uint32_t j = clz_below2(via2 ? wm2 : wm1, 128);
-                superseded[j >> 6] |= 1ull << (j & 63);
-                const uint32_t js = j >> 6, jl = j & 63;
-                uint32_t pj[kCmpW];
-#pragma unroll
-                for (int i = 0; i < kCmpW; i++)
-                    pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(jl << 2), (int)(js ? X[1].pw[i] : X[0].pw[i]));
-                // lane cl of set cs is decided again: candidate ip + j
-#pragma unroll
-                for (int st = 0; st < 2; st++) {
-                    if (st != (int)cs)
-                        continue;
-                    uint32_t mc = first_diff<kCmpW>(pj, X[st].pw);
-                    mc = mc < n - p[st] ? mc : n - p[st];
-                    const bool isc = l == cl;
-                    X[st].ok = isc ? ((pj[0] ^ X[st].pw[0]) & 0xFFFFFFu) == 0 : X[st].ok;
-                    X[st].mlen = isc ? mc : X[st].mlen;
-                    X[st].cand = isc ? ip + j : X[st].cand;
-                    X[st].slot = isc ? (via2 ? X[st].h2 : X[st].h1) : X[st].slot;
-                    X[st].use2 = isc ? via2 : X[st].use2;
-                    um2[st] = via2 ? um2[st] | (1ull << cl) : um2[st] & ~(1ull << cl);
-                    okm[st] = wave_ballot(X[st].ok);
-                }
-                keep_below2(path, c);
-                keep_below2(mstart, c);
-                nmatch = (uint32_t)__builtin_popcountll(mstart[0]) + (uint32_t)__builtin_popcountll(mstart[1]);
-                walk(c);
-            }
-            uint64_t keep[2] = {~0ull, ~0ull};
-            keep_below2(keep, end >= 128 ? 128u : end);
-
-            uint32_t npw[2][kCmpW];
-            load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw[0]);
-            load_at<kCmpW, POM_PW_AUX>(B, ip + end + kWave + l, npw[1]);
-
-            // ---- tokens for the matches before the cut ---------------------
-            uint64_t km[2] = {mstart[0] & keep[0], mstart[1] & keep[1]};
-            uint64_t dm[2];
-#pragma unroll
-            for (int st = 0; st < 2; st++)
-                dm[st] = km[st] & mask_ge(p[st] + X[st].mlen, ip_end);
-            const bool done = dm[0] || dm[1];
-            if (done) {
-                const uint32_t d = ctz2(dm, 0);
-                keep_below2(km, d + 1);
-            }
-            if (km[0] || km[1]) {
-                const uint32_t cnt = (uint32_t)__builtin_popcountll(km[0]) + (uint32_t)__builtin_popcountll(km[1]);
-                if (tp + cnt - E->ct > kTok)
-                    E->drain(tp);
-                uint64_t stopm[2] = {~(path[0] & ~mstart[0]), ~(path[1] & ~mstart[1])};
-#pragma unroll
-                for (int st = 0; st < 2; st++) {
-                    const uint32_t v = kWave * st + l;
-                    const uint32_t sb = clz_below2(stopm, v);
-                    const uint32_t from = sb != 0xFFFFFFFFu ? ip + sb + 1 : ii;
-                    const uint32_t r = popc_below2(km, v);
-                    S.tok[(km[st] >> l) & 1ull ? (tp + r) % kTok : kTok] =
-                        make_uint4(from, p[st] - from, X[st].mlen, p[st] - X[st].cand);
-                }
-                tp += cnt;
-                lds_store(&S.prod, tp);
-                const uint32_t last = clz_below2(km, 128);
-                ii = ip + last + lane_read(last >> 6 ? X[1].mlen : X[0].mlen, last & 63);
-                if (tp - E->ct >= POM_ENC_DRAIN)
-                    E->drain(tp);
-            }
-            // UPDATE_I of every path lane before the cut but the superseded ones
-#pragma unroll
-            for (int st = 0; st < 2; st++)
-                if ((path[st] & keep[st] & ~superseded[st]) >> l & 1ull)
-                    D.put(X[st].slot, p[st] - base + 1);
-            wave_order();
-            if (done)
-                break;
-            ip += end;
-            if (ip >= ip_end)
-                break;
-#pragma unroll
-            for (int st = 0; st < 2; st++)
-#pragma unroll
-                for (int i = 0; i < kCmpW; i++)
-                    X[st].pw[i] = npw[st][i];
-        }
-    }
-    // tail + EOF
-    if (tp - E->ct >= kTok)
-        E->drain(tp);
-    if (l == 0)
-        S.tok[tp % kTok] = make_uint4(ii, n - ii, 0, 0);
-    tp++;
-    lds_store(&S.prod, tp);
-    E->drain(tp);                                    // through the tail: out_len, status set
-    if (pf_acc == 0x9E3779B9u)                       // (keeps the prefetch loads; never matters)
-        S.sink = pf_acc;
-}
-
 // Emit wave (two-wave kernels): drains the token queue as the parse wave
 // fills it.
 template <bool GD>
@@ -1376,44 +1025,6 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
     }
 }
 
-// The one-wave global-dictionary encoder with 128-position windows
-// (parse_wave_w2; debug key enc_w2=1).
-__global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdict1w_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
-    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
-    uint8_t* __restrict__ dicts)
-{
-    __shared__ EncLdsT<true> S;
-    Dict<true> D;
-    D.lds = nullptr;
-    D.g = (gu16*)(dicts + kScratchHead + (size_t)blockIdx.x * kDictBytes);
-    const uint32_t l = lane_id();
-    const bool dyn = nblocks > gridDim.x;
-    for (uint32_t b = blockIdx.x; b < nblocks; b = dyn ? next_block((uint32_t*)dicts) : nblocks) {
-        const uint32_t n = src_len[b];
-        if (n > kMaxN) {
-            if (l == 0)
-                status[b] = LZO_MI355X_ENC_PENDING;
-            continue;
-        }
-        const uint8_t* in = src + src_off[b];
-        Emitter<true> E(S, in, n, dst + dst_off[b], dst_cap[b]);
-        E.olen = out_len;
-        E.ost = status;
-        E.blk = b;
-        E.prio = !dyn;
-        if (threadIdx.x == 0) {
-            S.prod = 0;
-            S.cons = 0;
-        }
-        wave_order();
-        parse_wave_w2(S, D, in, n, l, &E);
-        wave_order();
-    }
-}
-
 }  // namespace
 
 // Waves per block of the global-dictionary encoder: debug key enc_waves of
@@ -1469,10 +1080,7 @@ extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_
     const uint32_t grid = scratch ? enc_grid(scratch_bytes, nblocks) : 0u;
     if (grid && grid < nblocks && hipMemsetAsync(scratch, 0, sizeof(uint32_t), stream) != hipSuccess)
         return -1;                                   // (the block ticket)
-    if (grid && enc_waves() == 1 && pom_dbg_int("enc_w2", 0) == 1)
-        hipLaunchKernelGGL(lzo1x_encode_gdict1w_kernel, dim3(grid), dim3(kWave), 0, stream, src, src_off,
-                           src_len, dst, dst_off, dst_cap, out_len, status, nblocks, (uint8_t*)scratch);
-    else if (grid && enc_waves() == 1)
+    if (grid && enc_waves() == 1)
         hipLaunchKernelGGL(lzo1x_encode_gdict1_kernel, dim3(grid), dim3(kWave), 0, stream, src, src_off,
                            src_len, dst, dst_off, dst_cap, out_len, status, nblocks, (uint8_t*)scratch);
     else if (grid)

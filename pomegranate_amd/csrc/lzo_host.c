@@ -31,7 +31,7 @@
  * a comma-separated list of key=value.  No product path
  * needs it; an unset key takes its default.  Keys: decoder=fast|win
  * (device batches), sc_copy=1, sc_combine=0, sc_lat=0, sc_lat_min=BYTES,
- * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, enc_lds_max=N, enc_waves=1|2, enc_w2=1,
+ * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, enc_lds_max=N, enc_waves=1|2,
  * enc_grid=N.  Read at every use (tests change it between calls). */
 const char *pom_dbg_str(const char *key, char *buf, size_t n)
 {

@@ -573,17 +573,14 @@ def test_host_batch_api_many_mixed_blocks(dev, oracle):
     assert outs == blocks
 
 
-@pytest.mark.parametrize("kernel", ["gdict_one_wave", "gdict_two_wave", "lds", "gdict_w2", "gdict_w2_far"])
+@pytest.mark.parametrize("kernel", ["gdict_one_wave", "gdict_two_wave", "lds"])
 def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
     """Each throughput encoder kernel (global dictionary with one or two waves
-    per block or with 128-position windows, LDS dictionary) byte-identical to
-    the oracle on the sweep's content models, sizes up to 300 KB, more blocks
-    than one grid holds (and, for the 128-position windows, the far-repeat
-    blocks of _far_blocks)."""
-    waves = {"gdict_two_wave": "enc_waves=2", "gdict_w2": "enc_waves=1,enc_w2=1",
-             "gdict_w2_far": "enc_waves=1,enc_w2=1"}.get(kernel, "enc_waves=1")
+    per block, LDS dictionary) byte-identical to the oracle on the sweep's
+    content models, sizes up to 300 KB, more blocks than one grid holds."""
+    waves = "enc_waves=2" if kernel == "gdict_two_wave" else "enc_waves=1"
     monkeypatch.setenv("POM_LZO_DEBUG", waves)          # (lzo_host.c pom_dbg_str)
-    blocks = _far_blocks() if kernel == "gdict_w2_far" else _sweep_blocks(300, 91)
+    blocks = _sweep_blocks(300, 91)
     src = gu.device_batch(torch, blocks, dev, shift=1)
     dst = gu.empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
     olen = torch.zeros(len(blocks), dtype=torch.int32, device=dev)
@@ -594,7 +591,7 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
         # a grid of 40 workgroups: each dictionary region serves several blocks,
         # taken through the block ticket (scratch sized for the batch, as the
         # ABI requires; its ticket word starts as garbage)
-        monkeypatch.setenv("POM_LZO_DEBUG", waves + (",enc_grid=40" if len(blocks) > 40 else ",enc_grid=5"))
+        monkeypatch.setenv("POM_LZO_DEBUG", waves + ",enc_grid=40")
         scr = torch.full((lzo.compress_scratch_bytes(len(blocks)),), 0x5A, dtype=torch.uint8, device=dev)
         lzo.compress_dev(src, dst, olen, st, scratch=scr)
     torch.cuda.synchronize()
