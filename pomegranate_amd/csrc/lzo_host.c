@@ -28,7 +28,7 @@
 #include "minilzo.h"
 
 /* Debug and experiment switches: ONE environment variable, POM_LZO_DEBUG,
- * a comma-separated list of key=value (INTEGRATION.md 6).  No product path
+ * a comma-separated list of key=value (INTEGRATION.md section 6).  No product path
  * needs it; an unset key takes its default.  Keys: decoder=fast|win
  * (device batches), sc_copy=1, sc_combine=0, sc_lat=0, sc_lat_min=BYTES,
  * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, enc_lds_max=N, enc_waves=1|2,
