@@ -110,9 +110,12 @@ int pom_xnet_itb_wb_batch(uint8_t *const *itb, uint8_t *const *tmp, const size_t
                           const struct pom_xnet_wb *wb, size_t n, uint64_t site_id, uint64_t txg,
                           uint8_t magic, uint8_t *wire, size_t cap, size_t *wire_len, int *err);
 
-/* MDS: n received ITB replies.  Frame b's data is copied into itb[b] (a whole
- * ITB buffer of itb_cap bytes) and a COMPR_LZO record is decompressed in
- * place (pom_itb_lzo_decompress_batch, GPU).  err[b]:
+/* MDS: n received ITB replies.  Frame b's ITB lands in itb[b] (a whole ITB
+ * buffer of itb_cap bytes): an uncompressed record is copied; a COMPR_LZO
+ * record's header is copied and its payload decoded straight from the wire
+ * into itb[b] after the header (GPU), the header then left as
+ * itb_lzo_decompress leaves it (algo NONE, len = header + decoded bytes;
+ * mds/itb.c:2949-2980).  err[b]:
  *   0        the ITB in itb[b] is ready;
  *   -EBADMSG the frame was dropped (magic);
  *   -EIO     data longer than itb_cap, or tx.len != h.len;

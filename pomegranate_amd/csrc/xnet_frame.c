@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "lzo_mi355x.h"
 #include "lzo_mi355x_kernels.h"
 #include "minilzo.h"
 #include "pom_itb.h"
@@ -177,55 +178,76 @@ int pom_xnet_itb_wb_batch(uint8_t *const *itb, uint8_t *const *tmp, const size_t
     return rc;
 }
 
+/* The MDS load path for a batch of received messages: each message's ITB is
+ * checked (the load path's length ASSERT), an uncompressed one copied into its
+ * buffer, and a COMPR_LZO one decoded straight from the wire into its buffer
+ * after the header -- the compressed payload is never copied on the host --
+ * with the header then rewritten as itb_lzo_decompress leaves it
+ * (mds/itb.c:2949-2980: algo NONE, len = header + decoded bytes). */
 int pom_xnet_itb_recv_batch(const struct pom_xnet_frame *f, size_t n, uint8_t *const *itb,
                             size_t itb_cap, int *err)
 {
     if (n == 0)
         return 0;
-    uint8_t **dec = malloc(n * sizeof(*dec));
-    size_t *cap = malloc(n * sizeof(*cap));
+    const uint8_t **src = malloc(n * sizeof(*src));
+    size_t *slen = malloc(n * sizeof(*slen));
+    uint8_t **dst = malloc(n * sizeof(*dst));
+    size_t *dlen = malloc(n * sizeof(*dlen));
+    int *st = malloc(n * sizeof(*st));
     size_t *at = malloc(n * sizeof(*at));
-    int *derr = malloc(n * sizeof(*derr));
+    uint8_t **cdst = malloc(n * sizeof(*cdst));
     const uint8_t **csrc = malloc(n * sizeof(*csrc));
     size_t *clen = malloc(n * sizeof(*clen));
     int rc = LZO_E_OUT_OF_MEMORY;
-    if (!dec || !cap || !at || !derr || !csrc || !clen)
+    if (!src || !slen || !dst || !dlen || !st || !at || !cdst || !csrc || !clen)
         goto out;
-    /* the data of every frame into its ITB buffer (threaded copies) */
+    size_t nd = 0, nc = 0;
     for (size_t b = 0; b < n; b++) {
         const uint32_t len = f[b].tx.len;
         err[b] = f[b].dropped ? -EBADMSG : len < POM_ITBH_SIZE || len > itb_cap ? -EIO : 0;
-        csrc[b] = f[b].data;
-        clen[b] = err[b] ? 0 : len;
-    }
-    pom_copy_parallel(itb, csrc, clen, n);
-    size_t nd = 0;
-    for (size_t b = 0; b < n; b++) {
         if (err[b])
             continue;
-        const uint32_t len = f[b].tx.len;
-        if (rd32(itb[b] + POM_ITBH_LEN_OFF) != len) {   /* the load path's ASSERT */
+        const uint8_t *w = f[b].data;
+        if (rd32(w + POM_ITBH_LEN_OFF) != len) {      /* the load path's ASSERT */
             err[b] = -EIO;
             continue;
         }
-        if (rd16(itb[b] + POM_ITBH_ALGO_OFF) == POM_COMPR_LZO) {
-            dec[nd] = itb[b];
-            cap[nd] = itb_cap;
+        if (rd16(w + POM_ITBH_ALGO_OFF) == POM_COMPR_LZO) {
+            memcpy(itb[b], w, POM_ITBH_SIZE);
+            src[nd] = w + POM_ITBH_SIZE;
+            slen[nd] = len - POM_ITBH_SIZE;
+            dst[nd] = itb[b] + POM_ITBH_SIZE;
+            dlen[nd] = itb_cap - POM_ITBH_SIZE;
             at[nd] = b;
             nd++;
+        } else {
+            cdst[nc] = itb[b];
+            csrc[nc] = w;
+            clen[nc] = len;
+            nc++;
         }
     }
-    rc = pom_itb_lzo_decompress_batch(dec, cap, derr, NULL, nd);
+    pom_copy_parallel(cdst, csrc, clen, nc);
+    rc = nd ? lzo_mi355x_decompress_batch(src, slen, dst, dlen, st, nd) : LZO_E_OK;
     if (rc != LZO_E_OK)
         goto out;
-    for (size_t i = 0; i < nd; i++)
-        if (derr[i] != LZO_E_OK)
-            err[at[i]] = -EFAULT;                   /* itb_lzo_decompress failed */
+    for (size_t i = 0; i < nd; i++) {
+        uint8_t *h = itb[at[i]];
+        const uint16_t none = POM_COMPR_NONE;
+        const uint32_t nl = (uint32_t)(dlen[i] + POM_ITBH_SIZE);
+        memcpy(h + POM_ITBH_ALGO_OFF, &none, 2);      /* clear the compress flag */
+        memcpy(h + POM_ITBH_LEN_OFF, &nl, 4);
+        if (st[i] != LZO_E_OK)
+            err[at[i]] = -EFAULT;                     /* itb_lzo_decompress failed */
+    }
 out:
-    free(dec);
-    free(cap);
+    free(src);
+    free(slen);
+    free(dst);
+    free(dlen);
+    free(st);
     free(at);
-    free(derr);
+    free(cdst);
     free(csrc);
     free(clen);
     return rc;
