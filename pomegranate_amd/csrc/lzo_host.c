@@ -31,7 +31,7 @@
  * a comma-separated list of key=value.  No product path
  * needs it; an unset key takes its default.  Keys: decoder=fast|win
  * (device batches), sc_copy=1, sc_combine=0, sc_lat=0, sc_lat_min=BYTES,
- * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, enc_lds_max=N, enc_waves=1|2,
+ * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, dec_small_first=0, enc_lds_max=N, enc_waves=1|2,
  * enc_grid=N.  Read at every use (tests change it between calls). */
 const char *pom_dbg_str(const char *key, char *buf, size_t n)
 {
@@ -834,9 +834,9 @@ static int chunk_deliver(struct slot *S, struct layout *L, const struct hbatch *
  * the device's kSlots slots: chunk k is staged and its copies and kernels are
  * queued as soon as chunk k - kSlots has been waited for and unpacked, so the
  * copies, the kernels of several chunks and the host-side packing overlap.
- * The first chunk, the largest blocks, gets a quarter of the budget: their
- * long serial LZ chains start while the rest of the batch is still being
- * copied up.  Debug key chunk_mb overrides the budget. */
+ * The first chunk gets a quarter of the budget: for compress batches it holds
+ * the largest blocks, whose long serial LZ chains start while the rest of the
+ * batch is still being copied up; decode batches go smallest first (dev_run).  Debug key chunk_mb overrides the budget. */
 static const size_t kChunkBudget = (size_t)128 << 20;
 /* compress batches take twice that: their chains are long (a 536 KB ITB is
  * ~6 ms on one CU), so fewer, larger chunks all get in flight at once -- C5's
@@ -864,6 +864,18 @@ static int dev_run(void *arg, int d)
     } else {
         const size_t *ids = B->plan.by_dev + B->plan.dev_off[d];
         const size_t nids = B->plan.dev_off[d + 1] - B->plan.dev_off[d];
+        /* decode batches go smallest first: a decoded chunk's D2H copy is the
+         * long pole (PCIe), and the first chunk's kernels -- the smallest
+         * blocks -- finish early, so the copies start early and run back to
+         * back while the chunks of the largest blocks decode (debug key
+         * dec_small_first=0: largest first, as compress batches) */
+        size_t *rev = NULL;
+        if (B->kind != OP_COMPRESS && nids > 1 && pom_dbg_int("dec_small_first", 1) != 0 &&
+            (rev = malloc(nids * sizeof(*rev))) != NULL) {
+            for (size_t i = 0; i < nids; i++)
+                rev[i] = ids[nids - 1 - i];
+            ids = rev;
+        }
         struct layout L[kSlots];
         int live[kSlots] = {0};                /* slot holds a launched chunk */
         size_t from = 0;
@@ -913,6 +925,7 @@ static int dev_run(void *arg, int d)
                     break;
             }
         }
+        free(rev);
     }
     if (prev_dev != device)
         hipSetDevice(prev_dev);
