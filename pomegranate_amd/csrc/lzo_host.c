@@ -730,9 +730,20 @@ static int chunk_launch(struct slot *S, struct layout *L, const struct hbatch *B
     uint32_t *ol = (uint32_t *)(d + L->o_outlen);
     int32_t *st = (int32_t *)(d + L->o_status);
     int rc;
-    if (B->kind == OP_COMPRESS)
-        rc = lzo_mi355x_compress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb,
-                                     nb <= B->enc_lds_max ? NULL : d + L->o_scr, s);
+    if (B->kind == OP_COMPRESS) {
+        /* lzo_mi355x_compress_dev, with the general encoder's pass only when a
+         * block of the chunk needs it: that kernel's workgroups take 64 KB of
+         * LDS each, and behind the other slots' encoders a pass with nothing to
+         * do waited ~0.75 ms for LDS to free up (C5 trace) */
+        void *scr = nb <= B->enc_lds_max ? NULL : d + L->o_scr;
+        int big = 0;
+        for (size_t i = 0; i < L->nb; i++)
+            big |= B->src_len[L->ids[i]] > LZO_MI355X_FAST_MAX_N;
+        rc = lzo_mi355x_launch_compress_fast(dsrc, so, sl, ddst, dof, dc, ol, st, nb, scr,
+                                             scr ? lzo_mi355x_compress_scratch(nb) : 0, s);
+        if (rc == 0 && big)
+            rc = lzo_mi355x_launch_compress(dsrc, so, sl, ddst, dof, dc, ol, st, nb, 1, s);
+    }
     else if (B->kind == OP_DECOMPRESS) {
         const int lat = lat_chunk(S, L, h, d, s);
         rc = lat < 0 ? -1 : lat > 0 ? 0 : decompress_dev(dsrc, so, sl, ddst, dof, dc, ol, st, nb, d + L->o_scr, 0, s);

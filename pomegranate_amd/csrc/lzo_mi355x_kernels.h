@@ -14,6 +14,8 @@ extern "C" {
 /* status of a block lzo1x_encode_fast_kernel left to the general encoder */
 #define LZO_MI355X_ENC_PENDING 0x7FFF0002
 
+#define LZO_MI355X_FAST_MAX_N (1u << 24)   /* the throughput encoder's largest block (kMaxN) */
+
 /* Throughput encoder (lzo1x_encode_fast.hip), blocks of up to 16 MiB; larger
  * blocks get status LZO_MI355X_ENC_PENDING.  With scratch (scratch_bytes of
  * device memory, lzo_mi355x_compress_scratch()) the dictionaries live there
