@@ -1335,9 +1335,16 @@ static void sc_run_group(struct sc_req **g, int k, struct sc_queue *q)
     int32_t *ost = zc ? hh.status : dh.status;
     int rc;
     if (kind == SC_COMPRESS) {
-        /* no scratch: the LDS-dictionary encoder, faster for a few blocks */
-        rc = lzo_mi355x_compress_dev(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap, olen, ost,
-                                     (uint32_t)k, NULL, s);
+        /* no scratch: the LDS-dictionary encoder, faster for a few blocks; the
+         * general encoder's pass only for a block over 16 MiB */
+        int big = 0;
+        for (int i = 0; i < k; i++)
+            big |= g[i]->src_len > LZO_MI355X_FAST_MAX_N;
+        rc = lzo_mi355x_launch_compress_fast(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap, olen,
+                                             ost, (uint32_t)k, NULL, 0, s);
+        if (rc == 0 && big)
+            rc = lzo_mi355x_launch_compress(d, dh.src_off, dh.src_len, out, dh.dst_off, dh.dst_cap, olen, ost,
+                                            (uint32_t)k, 1, s);
     } else {
         /* SC_UNCHECKED: decoded into the room; the unchecked decoder never
          * reports an output overrun (lib/minilzo.c:3676-3680), so

@@ -431,6 +431,20 @@ def test_large_blocks_vs_oracle(dev, gu, oracle, n):
     assert st2 == [0] and outs[0] == blk
 
 
+def test_host_batch_and_single_call_past_16_mib_vs_oracle(dev, oracle):
+    """A block one byte past the throughput encoder's 16 MiB limit through the
+    host batch (a chunk of its own, the general encoder's pass launched because
+    of it, beside a small block) and through lzo1x_1_compress: byte-identical
+    to the oracle."""
+    blk = _large_block((16 << 20) + 1, 17)
+    small = synth.block(synth.ITB, 18, 65536)
+    rc, st, comps = lzo.compress_batch([blk, small])
+    assert rc == 0 and st == [0, 0]
+    assert comps[0] == oracle.compress(blk) and comps[1] == oracle.compress(small)
+    rc, z = lzo.lzo1x_1_compress(blk)
+    assert rc == 0 and z == comps[0]
+
+
 def test_blocks_past_32_mib_vs_oracle(dev, gu, oracle):
     """The general encoder keeps 25-bit dictionary positions relative to a
     base that moves up 16 MiB at a time; blocks of any length stay
