@@ -31,7 +31,7 @@
  * a comma-separated list of key=value.  No product path
  * needs it; an unset key takes its default.  Keys: decoder=fast|win
  * (device batches), sc_copy=1, sc_combine=0, sc_lat=0, sc_lat_min=BYTES,
- * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, dec_small_first=0, enc_lds_max=N, enc_waves=1|2,
+ * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, dec_small_first=0, ooo=0, enc_lds_max=N, enc_waves=1|2,
  * enc_grid=N.  Read at every use (tests change it between calls). */
 const char *pom_dbg_str(const char *key, char *buf, size_t n)
 {
@@ -581,6 +581,7 @@ struct hbatch {
     struct tctx *t;
     uint32_t enc_lds_max;   /* chunks of at most this many blocks: LDS dictionaries */
     int nslots;             /* chunks in flight per device (<= kSlots) */
+    int ooo;                /* deliver chunks in completion order (compress batches) */
     pom_chunk_fn on_chunk;  /* called with each delivered chunk's block ids, or NULL */
     pom_chunk_fn pre_chunk; /* called with a chunk's block ids before its inputs are staged */
     void *cb_ctx;
@@ -849,15 +850,32 @@ static int chunk_deliver(struct slot *S, struct layout *L, const struct hbatch *
  * the largest blocks, whose long serial LZ chains start while the rest of the
  * batch is still being copied up; decode batches go smallest first (dev_run).  Debug key chunk_mb overrides the budget. */
 static const size_t kChunkBudget = (size_t)128 << 20;
-/* compress batches take twice that: their chains are long (a 536 KB ITB is
- * ~6 ms on one CU), so fewer, larger chunks all get in flight at once -- C5's
- * 1,024 records compress at 17.5 against 14.5 GiB/s (PCIe included) with 256
- * against 128 MiB; decode batches are faster with 128 (25.2 against 23.0 GiB/s
- * read), where the copies are the larger share (profiles/r04b) */
-static const size_t kChunkBudgetCompress = (size_t)256 << 20;
+/* compress batches: their chains are long (a 536 KB ITB is ~6 ms on one CU),
+ * so their chunks are delivered in completion order (hbatch.ooo): a chunk of
+ * smaller blocks that finishes while the largest blocks' chunk still runs
+ * frees its slot for the next chunk and is handed to on_chunk (the append
+ * file) at once.  In launch order, 128 MiB chunks left the slots waiting on
+ * the first chunk (C5 compress 13.4-14.7 against 16.4-17.7 GiB/s with 256
+ * MiB); in completion order they compress as fast and the fused write gains
+ * (profiles/r04e/c5_ooo/) */
+static const size_t kChunkBudgetCompress = (size_t)128 << 20;
 static const size_t kChunkBlocks = (size_t)1 << 20;
 /* below this many bytes per device a batch stays on one device */
 static const size_t kSplitMinBytes = (size_t)64 << 20;
+
+/* Completion order (compress batches, hbatch.ooo): the first live slot whose
+ * stream is done, polling every 20 us; a failed stream counts as done (its
+ * delivery reports the error). */
+static int wait_any_done(struct dctx *c, const int *live, int nslots)
+{
+    for (;;) {
+        for (int i = 0; i < nslots; i++)
+            if (live[i] && hipStreamQuery(c->s[i].stream) != hipErrorNotReady)
+                return i;
+        const struct timespec ts = {0, 20000};
+        nanosleep(&ts, NULL);
+    }
+}
 
 static int dev_run(void *arg, int d)
 {
@@ -891,22 +909,43 @@ static int dev_run(void *arg, int d)
         int live[kSlots] = {0};                /* slot holds a launched chunk */
         size_t from = 0;
         for (int k = 0;; k++) {
-            const int cur = k % B->nslots, nxt = (k + 1) % B->nslots;
+            int cur = k % B->nslots;
+            const int nxt = (k + 1) % B->nslots;
             const size_t *done_ids = NULL;     /* the chunk delivered now, for on_chunk */
             size_t done_nb = 0;
-            if (live[cur]) {                   /* chunk k - nslots: wait, unpack */
-                if (chunk_deliver(&c->s[cur], &L[cur], B, live[nxt] ? &c->s[nxt] : NULL,
-                                  &L[nxt]) != 0) {
+            int dj = -1;                       /* slot to deliver now, if any */
+            if (!B->ooo) {
+                if (live[cur])                 /* chunk k - nslots: wait, unpack */
+                    dj = cur;
+            } else {
+                /* completion order: launch into a free slot; when there is
+                 * none, or nothing is left to launch, deliver whichever chunk
+                 * finishes first */
+                cur = -1;
+                for (int j = 0; j < B->nslots && cur < 0; j++)
+                    if (!live[j])
+                        cur = j;
+                int any = 0;
+                for (int j = 0; j < B->nslots; j++)
+                    any |= live[j];
+                if (any && (cur < 0 || from >= nids || rc != 0))
+                    dj = wait_any_done(c, live, B->nslots);
+            }
+            if (dj >= 0) {
+                const int ahead = !B->ooo && live[nxt] && nxt != dj;
+                if (chunk_deliver(&c->s[dj], &L[dj], B, ahead ? &c->s[nxt] : NULL, &L[nxt]) != 0) {
                     rc = -1;
                     for (int j = 0; j < B->nslots; j++)
                         hipStreamSynchronize(c->s[j].stream);
                 } else {
-                    done_ids = L[cur].ids;     /* (points into the plan, not the layout) */
-                    done_nb = L[cur].nb;
+                    done_ids = L[dj].ids;      /* (points into the plan, not the layout) */
+                    done_nb = L[dj].nb;
                 }
-                live[cur] = 0;
+                live[dj] = 0;
+                if (cur < 0)
+                    cur = dj;
             }
-            const int more = from < nids && rc == 0;
+            const int more = from < nids && rc == 0 && cur >= 0;
             if (more) {
                 const size_t end = pom_chunk_end(ids, from, nids, B->cost,
                                                  k ? B->budget : B->budget / 4, kChunkBlocks);
@@ -928,7 +967,7 @@ static int dev_run(void *arg, int d)
              * and kernels are in flight */
             if (done_ids && B->on_chunk)
                 B->on_chunk(B->cb_ctx, done_ids, done_nb);
-            if (!more) {
+            if (!(from < nids && rc == 0)) {
                 int any = 0;
                 for (int j = 0; j < B->nslots; j++)
                     any |= live[j];
@@ -1039,7 +1078,8 @@ static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const s
     }
     struct hbatch B = {kind, src, src_len, dst, dst_len, status, cap, cost,
                        kind == OP_COMPRESS ? kChunkBudgetCompress : kChunkBudget,
-                       {0, 1, NULL, NULL}, devs, t, 0, kSlots, on_chunk, pre_chunk, cb_ctx};
+                       {0, 1, NULL, NULL}, devs, t, 0, kSlots, 0, on_chunk, pre_chunk, cb_ctx};
+    B.ooo = kind == OP_COMPRESS && pom_dbg_int("ooo", 1) != 0;
     /* compress chunks that fit the LDS encoder's 4 blocks per CU at once use
      * it: a block alone on its CU finishes twice as fast as with the
      * dictionaries in HBM (that encoder wins only on full GPUs: 16 per CU) */
