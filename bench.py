@@ -118,173 +118,107 @@ def _ref_lib():
     return lib
 
 
+def _cpu_bench(plain, comps, threads, seconds):
+    """oracle/cpu_bench (native pthreads, no Python in the loop) on the sample:
+    lib/minilzo.c from oracle/_ref, else the oracle port.  Returns its JSON."""
+    import struct
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "oracle", "cpu_bench")
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libminilzo_ref.so")
+    lib = ref_path if os.path.exists(ref_path) else os.path.join(ROOT, "oracle", "liboracle.so")
+    if not os.path.exists(exe):
+        return None
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    path = os.path.join(d, f"pom_cpu_sample_{os.getpid()}.bin")
+    with open(path, "wb") as f:
+        f.write(struct.pack("<I", len(plain)))
+        for p_, z_ in zip(plain, comps):
+            f.write(struct.pack("<II", len(p_), len(z_)))
+            f.write(p_)
+            f.write(z_)
+    try:
+        r = subprocess.run([exe, lib, path, str(threads), str(seconds)], capture_output=True,
+                           text=True, timeout=seconds + 120)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu_bench failed ({r.returncode}): {r.stderr.strip()[:200]}")
+    return json.loads(r.stdout)
+
+
+def _leg(j, roundtrip=True):
+    c, d = j["compress_Bps"] / GIB, j["decompress_Bps"] / GIB
+    rt = 1.0 / (1.0 / c + 1.0 / d) if roundtrip else d
+    return {"value": round(rt, 4), "compress_value": round(c, 4), "decompress_value": round(d, 4),
+            "threads": j["threads"], "seconds": round(j["decompress_s"] + j["compress_s"], 1),
+            "per_thread_compress_GiBps": [round(x / GIB, 3) for x in j["per_thread_compress_Bps"]],
+            "per_thread_decompress_GiBps": [round(x / GIB, 3) for x in j["per_thread_decompress_Bps"]]}
+
+
 def cpu_c1(synth, seconds):
     """configs[0] (C1): lib/minilzo.c compress -> decompress round trip of
-    random 64 KiB blocks (xorshift64, seed 42 + b) on the host cores, a
-    bounded sample (the full 1 K blocks take minutes at ~0.08 GiB/s/core)."""
-    from concurrent.futures import ThreadPoolExecutor
+    random 64 KiB blocks (xorshift64, seed 42 + b) on the box's share of host
+    cores, through the native harness (oracle/cpu_bench)."""
     lib = _ref_lib()
     if lib is None:
         return None
     threads = host_cores()
-    blocks = [synth.block(synth.RANDOM, 42 + b, 65536) for b in range(max(threads, 16))]
-    ulong = ctypes.c_ulong
-
-    def share(t, deadline, res):
-        wrk = ctypes.create_string_buffer(131072)
-        z = ctypes.create_string_buffer(65536 + 65536 // 16 + 128)
-        o = ctypes.create_string_buffer(65536 + 64)
-        tc = td = 0.0
-        done = 0
-        b = t
-        while time.perf_counter() < deadline:
-            src = blocks[b % len(blocks)]
-            zl, ol = ulong(0), ulong(0)
-            t0 = time.perf_counter()
-            ctypes.memset(wrk, 0, 131072)
-            lib.lzo1x_1_compress(src, len(src), z, ctypes.byref(zl), wrk)
-            t1 = time.perf_counter()
-            rc = lib.lzo1x_decompress(z, zl.value, o, ctypes.byref(ol), None)
-            t2 = time.perf_counter()
-            assert rc == 0 and ol.value == len(src) and o.raw[: ol.value] == src
-            tc += t1 - t0
-            td += t2 - t1
-            done += len(src)
-            b += threads
-        res[t] = (done, tc, td)
-
-    res = [None] * threads
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(lambda t: share(t, t0 + seconds, res), range(threads)))
-    wall = time.perf_counter() - t0
-    n = sum(r[0] for r in res)
-    tc = sum(r[1] for r in res) / threads
-    td = sum(r[2] for r in res) / threads
-    return {"roundtrip_value": round(n / wall / GIB, 4), "unit": "GiB/s", "cores": threads,
-            "compress_value": round(n / threads / tc / GIB * threads, 4) if tc else None,
-            "decompress_value": round(n / threads / td / GIB * threads, 4) if td else None,
-            "kind": "reference",
-            "sample": f"configs[0]: random 64 KiB blocks (seed 42+b) compressed and decompressed "
-                      f"by lib/minilzo.c (oracle/_ref) on {threads} threads for {seconds:.0f} s "
-                      f"({int(n) >> 16} blocks)"}
-def cpu_baseline(plain, comps, seconds, roundtrip=True):
-    """Reference lib/minilzo.c (oracle/_ref) or, if absent, the oracle port, on
-    the host cores: decompress (and compress) of a bounded sample.  The
-    reference's compressed bytes of every sample block are compared with the
-    GPU's (C3 byte identity)."""
-    from concurrent.futures import ThreadPoolExecutor
-
-    ref_path = os.path.join(ROOT, "oracle", "_ref", "libminilzo_ref.so")
-    port_path = os.path.join(ROOT, "oracle", "liboracle.so")
-    ulong = ctypes.c_ulong
-    if os.path.exists(ref_path):
-        lib = ctypes.CDLL(ref_path)
-        kind = "reference"
-        dec = lib.lzo1x_decompress
-        comp = lib.lzo1x_1_compress
-        for f in (dec, comp):
-            f.restype = ctypes.c_int
-            f.argtypes = [ctypes.c_void_p, ulong, ctypes.c_void_p, ctypes.POINTER(ulong),
-                          ctypes.c_void_p]
-        init = getattr(lib, "__lzo_init_v2")
-        init(0x2040, 2, 4, 8, 4, 8, 8, 8, 8, 48)
-    else:
-        lib = ctypes.CDLL(port_path)
-        kind = "port"
-        dec = None
-        comp = None
-    threads = affinity_cpus()
-    nsample = len(plain)
-    lens = [len(p) for p in plain]
-    srcs = [ctypes.create_string_buffer(comps[b], len(comps[b]) + 64) for b in range(nsample)]
-
-    def compress_one(src, out, wrk):
-        ol = ulong(0)
-        if kind == "reference":
-            ctypes.memset(wrk, 0, 131072)
-            comp(src, len(src), out, ctypes.byref(ol), wrk)
-            return out.raw[: ol.value]
-        sz = ctypes.c_size_t(0)
-        lib.oracle_lzo1x_1_compress(src, ctypes.c_size_t(len(src)), out, ctypes.byref(sz))
-        return out.raw[: sz.value]
-
-    # C3: byte identity of the GPU's compressed blocks on the sample
-    out = ctypes.create_string_buffer(max(lens) * 2 + 128)
+    plain = [synth.block(synth.RANDOM, 42 + b, 65536) for b in range(64)]
+    comps = []
     wrk = ctypes.create_string_buffer(131072)
-    identical = sum(compress_one(plain[b], out, wrk) == comps[b] for b in range(nsample))
+    z = ctypes.create_string_buffer(65536 + 65536 // 16 + 128)
+    for p_ in plain:
+        zl = ctypes.c_ulong(0)
+        ctypes.memset(wrk, 0, 131072)
+        lib.lzo1x_1_compress(p_, len(p_), z, ctypes.byref(zl), wrk)
+        comps.append(z.raw[: zl.value])
+    j = _cpu_bench(plain, comps, threads, seconds)
+    leg = _leg(j)
+    return {"roundtrip_value": leg["value"], "unit": "GiB/s", "cores": threads,
+            "compress_value": leg["compress_value"], "decompress_value": leg["decompress_value"],
+            "kind": j["kind"],
+            "sample": f"configs[0]: 64 random 64 KiB blocks (seed 42+b), lib/minilzo.c (oracle/_ref) "
+                      f"on {threads} pinned threads of oracle/cpu_bench for {seconds:.0f} s "
+                      f"(decompress 60 %, then compress 40 %)"}
 
-    def dec_share(t, deadline, nbytes):
-        o = ctypes.create_string_buffer(max(lens) + 64)
-        done = 0
-        b = t
-        while time.perf_counter() < deadline:
-            ol = ulong(0)
-            if kind == "reference":
-                rc = dec(srcs[b], len(comps[b]), o, ctypes.byref(ol), None)
-            else:
-                sz = ctypes.c_size_t(len(o))
-                rc = lib.oracle_lzo1x_decompress_safe(srcs[b], ctypes.c_size_t(len(comps[b])),
-                                                      o, ctypes.byref(sz))
-            assert rc == 0
-            done += lens[b]
-            b = (b + threads) % nsample
-        nbytes[t] = done
 
-    def comp_share(t, deadline, nbytes):
-        o = ctypes.create_string_buffer(max(lens) * 2 + 128)
-        w = ctypes.create_string_buffer(131072)
-        done = 0
-        b = t
-        while time.perf_counter() < deadline:
-            compress_one(plain[b], o, w)
-            done += lens[b]
-            b = (b + threads) % nsample
-        nbytes[t] = done
-
-    def measure(nthr, secs):
-        res = {}
-        for name, fn, share in (("decompress", dec_share, 0.6), ("compress", comp_share, 0.4)):
-            nbytes = [0] * nthr
-            t0 = time.perf_counter()
-            deadline = t0 + secs * share
-            with ThreadPoolExecutor(nthr) as ex:
-                list(ex.map(lambda t: fn(t, deadline, nbytes), range(nthr)))
-            dt = time.perf_counter() - t0
-            res[name] = sum(nbytes) / dt / GIB
-        # the bench metric itself -- the round trip (compress then decompress of
-        # every byte on the same cores: 1 / (1/compress + 1/decompress)), or
-        # decompress for the decode-only C2 line; both legs beside it
-        rt = 1.0 / (1.0 / res["compress"] + 1.0 / res["decompress"]) if roundtrip else res["decompress"]
-        return {"value": round(rt, 4), "compress_value": round(res["compress"], 4),
-                "decompress_value": round(res["decompress"], 4), "seconds": round(secs, 1)}
-
-    # one thread per CPU of the affinity set (the headline), the box's
-    # OMP_NUM_THREADS share and one core beside it (BASELINE.md §2)
-    counts = []
-    for c in (threads, host_cores(), 1):
+def cpu_baseline(plain, comps, seconds, roundtrip=True):
+    """The reference's lib/minilzo.c (oracle/_ref; the oracle port if absent)
+    timed by oracle/cpu_bench -- native threads pinned one per CPU, per-thread
+    wrkmem and buffers, no Python in the loop -- on the same blocks the GPU
+    coded (their compressed bytes are the GPU's: the harness checks the
+    reference reproduces each one, C3 byte identity).  `value` and `cores` are
+    the box's CPU share (OMP_NUM_THREADS, 16 on the GPU box), a fixed, stated
+    core count; one core and the whole affinity set are beside it."""
+    share = host_cores()
+    counts = [share]
+    for c in (1, affinity_cpus()):
         if c not in counts:
             counts.append(c)
-    by = {str(c): measure(c, seconds if c == threads else seconds / 2) for c in counts}
-    # the headline is the fastest of them (on a box whose CPU share is smaller
-    # than its affinity set, one thread per CPU oversubscribes the share)
-    best = max(counts, key=lambda c: by[str(c)]["value"])
-    top = by[str(best)]
-    return {"value": top["value"], "unit": "GiB/s", "cores": best,
-            "affinity_cpus": threads,
-            "host": host_cpu_info(),
-            "kind": kind, "compress_value": top["compress_value"],
+    runs = {}
+    for c in counts:
+        runs[c] = _cpu_bench(plain, comps, c, seconds if c == share else seconds / 2)
+    if runs[share] is None:
+        return None
+    by = {str(c): _leg(j, roundtrip) for c, j in runs.items()}
+    top, one = by[str(share)], by["1"]
+    j = runs[share]
+    return {"value": top["value"], "unit": "GiB/s", "cores": share,
+            "affinity_cpus": affinity_cpus(), "host": host_cpu_info(),
+            "kind": j["kind"], "compress_value": top["compress_value"],
             "decompress_value": top["decompress_value"],
-            "by_threads": by,
-            "one_core": by["1"],
-            "byte_identical_blocks": f"{identical}/{nsample}",
-            "sample": f"{nsample} of the same {lens[0]}-byte ITB blocks, round-robin over "
-                      f"{threads} threads (one per CPU of the affinity set) for {seconds:.0f} s "
-                      f"(decompress {0.6 * seconds:.0f} s, compress {0.4 * seconds:.0f} s), "
-                      f"then on {', '.join(str(c) for c in counts[1:])} thread(s) for "
-                      f"{seconds / 2:.0f} s each (by_threads); value and cores: the fastest; "
+            "scaling_vs_one_core": {"compress": round(top["compress_value"] / one["compress_value"], 2),
+                                    "decompress": round(top["decompress_value"] / one["decompress_value"], 2)},
+            "by_threads": by, "one_core": one,
+            "byte_identical_blocks": f"{j['byte_identical']}/{j['blocks']}",
+            "harness": "oracle/cpu_bench.c (pthreads, pinned, wrkmem reused per thread as mds/itb.c:2913)",
+            "sample": f"{len(plain)} of the same {len(plain[0])}-byte ITB blocks, round-robin over "
+                      f"{share} pinned threads (the box's OMP_NUM_THREADS share) for {seconds:.0f} s "
+                      f"(decompress 60 %, then compress 40 %); 1 thread and the {affinity_cpus()}-CPU "
+                      f"affinity set for {seconds / 2:.0f} s each (by_threads); "
                       + ("lib/minilzo.c built from the reference sources (oracle/_ref)"
-                         if kind == "reference" else "oracle/lzo1x_oracle.c port")}
+                         if j["kind"] == "reference" else "oracle/lzo1x_oracle.c port")}
 
 
 KERNEL_SOURCES = {"decode": "pomegranate_amd/csrc/lzo1x_decode_fast.hip",
@@ -559,11 +493,13 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
     else:
         wall, (t_d,) = timed(torch, dist, world, stream, [R.decompress], args.steps, args.warmup)
         dec_wall, t_d2 = wall, t_d
-        _, (t_c,) = timed(torch, dist, world, stream, [R.compress], args.compress_steps, 1)
+        comp_wall, (t_c,) = timed(torch, dist, world, stream, [R.compress], args.compress_steps, 1)
         errors += int((R.ost != 0).sum().item()) + int((R.zst != 0).sum().item())
     if dist_on(dist):
         errors, wall = shard.completion_barrier(dist, dev, errors, wall)
         _, dec_wall = shard.completion_barrier(dist, dev, 0, dec_wall)
+        if args.workload != "c3":
+            _, comp_wall = shard.completion_barrier(dist, dev, 0, comp_wall)
         tot = torch.tensor([n_bytes, z_bytes], dtype=torch.float64,
                            device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tot)
@@ -614,6 +550,13 @@ def run_resident(args, torch, dist, lzo, synth, shard, dev, world, rank, backend
            "decode_frac": round((z_all + n_all) * args.steps / dec_wall / 1e9 / (world * HBM_PEAK_GBPS), 4)}
     if args.workload == "c3":
         agg["roundtrip_frac"] = round(2 * (z_all + n_all) * args.steps / wall / 1e9 / (world * HBM_PEAK_GBPS), 4)
+    else:
+        # the metric's own quantity on this workload: compress + decompress of
+        # every byte, whole job (each leg's max-over-ranks wall time per pass)
+        t_rt = comp_wall / args.compress_steps + dec_wall / args.steps
+        result["roundtrip_gibps"] = round(n_all / t_rt / GIB, 3)
+        result["compress_gibps"] = round(n_all * args.compress_steps / comp_wall / GIB, 3)
+        agg["roundtrip_frac"] = round(2 * (z_all + n_all) / t_rt / 1e9 / (world * HBM_PEAK_GBPS), 4)
     result["aggregate_hbm"] = agg
     copy = copy_gbps(torch, dev)
     for key in ("roofline", "compress_roofline"):
@@ -920,6 +863,11 @@ def run_others(args, torch, dist, lzo, synth, shard, dev, world, rank, backend):
         out["c4"] = {"workload": r["config"]["workload"], "n_gpus": world,
                      "blocks_per_gpu": r["config"]["blocks_per_gpu"],
                      "decompress_gibps": r["value"],             # all ranks' blocks / max rank time
+                     "compress_gibps": r["compress_gibps"],
+                     # compress + decompress of the 4-256 KiB blocks: the metric's
+                     # own wording (BASELINE.json), beside C3's `value`
+                     "roundtrip_gibps": r["roundtrip_gibps"],
+                     "aggregate_hbm": r["aggregate_hbm"],
                      "compress_kernel_gibps_rank0": r["compress_kernel_gibps"],
                      "step_ms_rank0": r["step_ms"], "compression_ratio": r["config"]["compression_ratio"],
                      "decode_roofline_frac_rank0": r["roofline"]["frac"], "errors": e}

@@ -128,6 +128,7 @@ struct Tok {
 };
 
 constexpr uint32_t kMaxExtZeros = 64;            // zero length-extension bytes a lane reads at most
+constexpr uint32_t kMaxRunZeros = 1u << 24;      // zero bytes the true path takes in one extension
 
 // One instruction at (pos, st), general form: long length extensions and
 // instructions that run past the staged piece (bytes read from HBM).  Bytes
@@ -146,10 +147,18 @@ __device__ __noinline__ Tok tok_slow(const WinLds& L, const Piece k, uint32_t po
     // scan the rest of it, for every start in the run; after kMaxExtZeros zero
     // bytes its guess is refused instead.  The true path -- the frontier,
     // counting and emitting walks -- scans each run once: linear time)
+    // (the true path too: a run of 2^24 zero bytes or more is refused, so the
+    // block goes to the exact decoder, which keeps the reference's 64-bit
+    // length, lib/minilzo.c:3805 -- from 16,843,009 zeros on, 255 per zero
+    // passes 2^32 and this u32 sum would wrap to a small, valid-looking length)
     bool capped = false;
     auto ext = [&](uint32_t& p, uint32_t base) -> uint32_t {
         uint32_t v = 0;
         while (p < k.z) {
+            if (v >= 255u * kMaxRunZeros) {
+                capped = true;
+                break;
+            }
             // (past the staged piece, aligned 16-byte reads take a long zero
             // run 16 bytes at a time: such a read never leaves the page of the
             // block's byte at p)

@@ -186,42 +186,86 @@ __device__ __forceinline__ void dec_back(Dec<WRITE>& d, uint32_t dist, uint32_t 
     }
 }
 
+// Lengths are 64-bit as the reference's lzo_uint t (lib/minilzo.c:3805): a
+// length extension of 16,843,009 zero bytes or more passes 2^32, which the
+// reference's NEED_OP / NEED_IP then refuse; 32 bits would wrap it small.
 template <bool WRITE>
-__device__ __forceinline__ bool dec_need_ip(const Dec<WRITE>& d, uint32_t x)
+__device__ __forceinline__ bool dec_need_ip(const Dec<WRITE>& d, uint64_t x)
 {
     // lib/minilzo.c:3733-3734: (lzo_uint)(ip_end - ip) < x; passes once ip > ip_end
     if (d.unchecked)
         return d.ip <= d.W.len + kUncheckedSlack;
-    return !(d.ip <= d.W.len && d.W.len - d.ip < x);
+    return !(d.ip <= d.W.len && (uint64_t)(d.W.len - d.ip) < x);
 }
 
 template <bool WRITE>
-__device__ __forceinline__ bool dec_need_op(const Dec<WRITE>& d, uint32_t x)
+__device__ __forceinline__ bool dec_need_op(const Dec<WRITE>& d, uint64_t x)
 {
-    return d.cap - d.op >= x;
+    return (uint64_t)(d.cap - d.op) >= x;
 }
 
+// Index of the first nonzero byte of in[from, len), or len if there is none.
+// Each lane tests one aligned 16-byte granule, 1 KiB of input per step (an
+// aligned granule holding a byte of the block never leaves that byte's page;
+// bytes outside [from, len) are masked off).
+__device__ uint32_t first_nonzero(const uint8_t* in, uint32_t len, uint32_t from)
+{
+    if (from >= len)
+        return len;
+    const uintptr_t base = (uintptr_t)in, lo = base + from, hi = base + len;
+    const uintptr_t g = lo & ~(uintptr_t)15;
+    for (uintptr_t s = g; s < hi; s += 16 * kWave) {
+        const uintptr_t a = s + 16 * (uintptr_t)lane_id();
+        uint32_t f = 0xFFFFFFFFu;
+        if (a < hi) {
+            const uint4 v = *(const uint4*)a;
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int i = 3; i >= 0; i--) {
+                const uintptr_t wa = a + 4 * i;
+                uint32_t x = w[i];
+                if (wa + 4 <= lo || wa >= hi)
+                    x = 0;
+                if (wa < lo && wa + 4 > lo)
+                    x &= ~0u << (uint32_t)(8 * (lo - wa));
+                if (wa < hi && wa + 4 > hi)
+                    x &= ~0u >> (uint32_t)(8 * (wa + 4 - hi));
+                f = x ? (uint32_t)(wa - base) + ((uint32_t)__builtin_ctz(x) >> 3) : f;
+            }
+        }
+        const uint64_t m = wave_ballot(f != 0xFFFFFFFFu);
+        if (m)
+            return lane_read(f, ctz64(m));
+    }
+    return len;
+}
+
+// Length extension (lib/minilzo.c:3860-3870, :3991-4001, :4035-4045): 255 per
+// zero byte, then base + the first nonzero byte.  The safe decoder's NEED_IP(1)
+// after each zero fails once the run reaches the input end; the unchecked one
+// reads zeros past the end until kUncheckedSlack -- both fail exactly when the
+// run has no nonzero byte before the end.  The run is scanned a wave-wide
+// kilobyte at a time.
 template <bool WRITE>
-__device__ __forceinline__ bool dec_ext(Dec<WRITE>& d, uint32_t base, uint32_t& t)
+__device__ __forceinline__ bool dec_ext(Dec<WRITE>& d, uint32_t base, uint64_t& t)
 {
     if (!dec_need_ip(d, 1))
         return false;
-    uint32_t v = 0;
-    while (win_byte(d.W, d.ip) == 0) {
-        v += 255;
-        d.ip++;
-        if (!dec_need_ip(d, 1))
-            return false;
-    }
-    t = v + base + win_byte(d.W, d.ip);
-    d.ip++;
+    uint32_t f = d.ip;
+    if (win_byte(d.W, d.ip) == 0)
+        f = first_nonzero(d.W.in, d.W.len, d.ip + 1);
+    if (f >= d.W.len)
+        return false;
+    t = 255ull * (f - d.ip) + base + win_byte(d.W, f);
+    d.ip = f + 1;
     return true;
 }
 
 template <bool WRITE>
 __device__ int dec_run(Dec<WRITE>& d)
 {
-    uint32_t t, dist, len;
+    uint64_t t, len;
+    uint32_t dist;
     int where;
     t = win_byte(d.W, 0);
     if (t > 17) {                                   // lib/minilzo.c:3357-3365
@@ -232,7 +276,7 @@ __device__ int dec_run(Dec<WRITE>& d)
         else {
             if (!dec_need_op(d, t)) return E_OUTPUT_OVERRUN;
             if (!dec_need_ip(d, t + 1)) return E_INPUT_OVERRUN;
-            dec_lits(d, t);
+            dec_lits(d, (uint32_t)t);
             where = 1;
         }
     } else
@@ -253,7 +297,7 @@ __device__ int dec_run(Dec<WRITE>& d)
                 return E_INPUT_OVERRUN;
             if (!dec_need_op(d, t + 3)) return E_OUTPUT_OVERRUN;
             if (!dec_need_ip(d, t + 4)) return E_INPUT_OVERRUN;
-            dec_lits(d, t + 3);
+            dec_lits(d, (uint32_t)t + 3);
             where = 1;
             continue;
         }
@@ -263,13 +307,13 @@ __device__ int dec_run(Dec<WRITE>& d)
                 where = 2;
                 continue;
             }
-            dist = 1 + 0x800 + (t >> 2) + (win_byte(d.W, d.ip++) << 2);
+            dist = 1 + 0x800 + (uint32_t)(t >> 2) + (win_byte(d.W, d.ip++) << 2);
             if (dist > d.op) return E_LOOKBEHIND_OVERRUN;
             if (!dec_need_op(d, 3)) return E_OUTPUT_OVERRUN;
             dec_back(d, dist, 3);
         } else if (where == 2) {                    // :3446-3646
             if (t >= 64) {
-                dist = 1 + ((t >> 2) & 7) + (win_byte(d.W, d.ip++) << 3);
+                dist = 1 + (uint32_t)((t >> 2) & 7) + (win_byte(d.W, d.ip++) << 3);
                 len = (t >> 5) + 1;
             } else if (t >= 32) {
                 len = t & 31;
@@ -281,7 +325,7 @@ __device__ int dec_run(Dec<WRITE>& d)
                 dist = 1 + ((lo | (hi << 8)) >> 2);
                 d.ip += 2;
             } else if (t >= 16) {
-                uint32_t dd = (t & 8) << 11;
+                uint32_t dd = (uint32_t)(t & 8) << 11;
                 len = t & 7;
                 if (len == 0 && !dec_ext(d, 7, len))
                     return E_INPUT_OVERRUN;
@@ -296,12 +340,12 @@ __device__ int dec_run(Dec<WRITE>& d)
                 }
                 dist = dd + 0x4000;
             } else {
-                dist = 1 + (t >> 2) + (win_byte(d.W, d.ip++) << 2);
+                dist = 1 + (uint32_t)(t >> 2) + (win_byte(d.W, d.ip++) << 2);
                 len = 2;
             }
             if (dist > d.op) return E_LOOKBEHIND_OVERRUN;
             if (!dec_need_op(d, len)) return E_OUTPUT_OVERRUN;
-            dec_back(d, dist, len);
+            dec_back(d, dist, (uint32_t)len);
         }
         if (where != 3) {                           // match_done, :3650-3653
             t = win_byte(d.W, d.ip - 2) & 3;
@@ -313,7 +357,7 @@ __device__ int dec_run(Dec<WRITE>& d)
         // match_next, :3654-3668
         if (!dec_need_op(d, t)) return E_OUTPUT_OVERRUN;
         if (!dec_need_ip(d, t + 1)) return E_INPUT_OVERRUN;
-        dec_lits(d, t);
+        dec_lits(d, (uint32_t)t);
         t = win_byte(d.W, d.ip++);
         if (!d.unchecked && !(d.ip < d.W.len))
             return E_EOF_NOT_FOUND;

@@ -130,6 +130,18 @@ def fwritev_columns():
 
 
 @pytest.fixture(scope="session")
+def longext():
+    """Streams with one length extension of 16,843,008-16,843,010 zero bytes
+    (255 per zero passes 2^32) and what the reference's lzo1x_decompress_safe
+    returns on them (tests/golden/make_golden.py longext_cases); the streams
+    are rebuilt from the spec."""
+    from tests.golden.make_golden import longext_stream
+    with open(os.path.join(GOLDEN, "longext.json")) as f:
+        cases = json.load(f)["cases"]
+    return [dict(c, stream=longext_stream(c["kind"], c["zeros"])) for c in cases]
+
+
+@pytest.fixture(scope="session")
 def manifest():
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         return json.load(f)["batches"]

@@ -258,6 +258,63 @@ def column_cases(ref: Ref):
     return {n: (r, l) for n, r, l in zip(names, rd_rc, rd_len)}
 
 
+def _ext(v: int, base: int) -> bytes:
+    """Length-extension bytes for v > base: zeros of 255 each, then the rest
+    (the encoder's side of lib/minilzo.c:3034-3046)."""
+    z, r = divmod(v - base, 255)
+    if r == 0:
+        z, r = z - 1, 255
+    return bytes(z) + bytes([r])
+
+
+def longext_stream(kind: str, zeros: int) -> bytes:
+    """A stream whose one length extension has `zeros` zero bytes then 0x01.
+
+    The bytes after it are laid out so that a decoder keeping the length in
+    32 bits -- 255 * 16,843,009 = 2^32 - 1 wraps -- reads a valid stream
+    ending in an EOF marker, while the reference's 64-bit lzo_uint t
+    (lib/minilzo.c:3805) sees a length past any room:
+      lit  literal run 0x00, ext (:3860-3871), wrapped-length literals, EOF
+      m3   4 literals, M3 0x20, ext (:3991-4001), distance 1, EOF
+      m4   4 literals, an M3 that makes 16,404 bytes of output, M4 0x10, ext
+           (:4035-4045), distance 0x4001, EOF
+    Built by tests/test_oracle.py and tests/test_gpu_codec.py from this spec;
+    the 16.8 MB streams themselves are not stored."""
+    wrap = lambda base: (255 * zeros + base + 1) % (1 << 32)
+    eof = bytes([0x11, 0, 0])
+    if kind == "lit":
+        t = wrap(15)                                           # (no wrap: no room anyway)
+        return b"\x00" + bytes(zeros) + b"\x01" + b"\x07" * ((t if t < 1 << 20 else 0) + 3) + eof
+    head = bytes([17 + 4]) + b"ABCD"
+    if kind == "m3":
+        return head + b"\x20" + bytes(zeros) + b"\x01" + b"\x00\x00" + eof
+    assert kind == "m4"
+    fill = b"\x20" + _ext(16400 - 2, 31) + b"\x00\x00"          # 16,400 bytes from distance 1
+    return head + fill + b"\x10" + bytes(zeros) + b"\x01" + b"\x04\x00" + eof
+
+
+LONGEXT_ZEROS = (16843008, 16843009, 16843010)
+LONGEXT_CAP = 1 << 20
+
+
+def longext_cases(ref: Ref):
+    """lzo1x_decompress_safe of the longext_stream()s: code, *out_len and the
+    SHA-256 of the produced bytes, room LONGEXT_CAP."""
+    cases = []
+    for kind in ("lit", "m3", "m4"):
+        for zeros in LONGEXT_ZEROS:
+            s = longext_stream(kind, zeros)
+            rc, out = ref.decompress_safe(s, LONGEXT_CAP)
+            cases.append({"kind": kind, "zeros": zeros, "stream_len": len(s), "cap": LONGEXT_CAP,
+                          "rc": rc, "out_len": len(out),
+                          "out_sha256": hashlib.sha256(out).hexdigest(),
+                          "stream_sha256": hashlib.sha256(s).hexdigest()})
+    with open(os.path.join(OUT, "longext.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py longext_cases",
+                   "reference": "lib/minilzo.c lzo1x_decompress_safe", "cases": cases}, f, indent=0)
+    return [(c["kind"], c["zeros"], c["rc"], c["out_len"]) for c in cases]
+
+
 def batch_entry(ref: Ref, name, model, seed0, sizes, note):
     arena, offs, lens = synth.batch(model, seed0, sizes)
     hz, hi = hashlib.sha256(), hashlib.sha256()
@@ -304,6 +361,7 @@ def main():
     print("unchecked rc histogram:", unchecked_cases(ref))
     print("column reader (rc, olen):", column_cases(ref))
     print("manifest:", manifest(ref))
+    print("long extensions:", longext_cases(ref))
 
 
 if __name__ == "__main__":

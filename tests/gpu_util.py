@@ -40,13 +40,17 @@ def empty_batch(torch, caps: Sequence[int], dev, fill: int = 0):
                            t(np.asarray(caps, np.uint32).view(np.int32)))
 
 
-def gpu_compress(torch, blocks: Sequence[bytes], dev, shift: int = 0):
+def gpu_compress(torch, blocks: Sequence[bytes], dev, shift: int = 0, scratch: bool = False):
+    """Device-batch compress.  Without scratch: the LDS-dictionary encoder;
+    with scratch: the global-dictionary one-wave encoder the bench times
+    (lzo1x_encode_gdict1_kernel)."""
     src = device_batch(torch, blocks, dev, shift)
     dst = empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
     n = len(blocks)
     olen = torch.zeros(n, dtype=torch.int32, device=dev)
     st = torch.full((n,), 99, dtype=torch.int32, device=dev)
-    lzo.compress_dev(src, dst, olen, st)
+    scr = torch.zeros(lzo.compress_scratch_bytes(n), dtype=torch.uint8, device=dev) if scratch else None
+    lzo.compress_dev(src, dst, olen, st, scratch=scr)
     torch.cuda.synchronize()
     return fetch(dst, olen), st.cpu().numpy().tolist()
 

@@ -97,6 +97,43 @@ def test_manifest_batches_round_trip(dev, gu, manifest, name):
     assert hashlib.sha256(b"".join(outs)).hexdigest() == entry["sha256_input"]
 
 
+@pytest.mark.parametrize("name", ["C1", "C2C3", "C4_sample", "itb_max", "random_300k"])
+def test_manifest_batches_bench_encoder(dev, gu, manifest, name):
+    """The same full-size batches through the encoder the bench times (device
+    batch with scratch: lzo1x_encode_gdict1_kernel, global dictionaries,
+    block tickets on C4's mixed sizes): compressed stream hashes to the
+    reference's."""
+    entry = next(e for e in manifest if e["name"] == name)
+    arena, offs, lens = synth.batch(entry["model_id"], entry["seed0"], batch_sizes(entry))
+    blocks = [arena[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+              for b in range(len(lens))]
+    comps, st = gu.gpu_compress(torch, blocks, dev, scratch=True)
+    assert all(s == 0 for s in st)
+    assert [len(c) for c in comps] == entry["zlens"]
+    assert hashlib.sha256(b"".join(comps)).hexdigest() == entry["sha256_z"]
+
+
+def test_long_extensions_past_32_bits(dev, longext):
+    """Length extensions of 16,843,008-16,843,010 zero bytes (255 per zero
+    passes 2^32 from 16,843,009 on): lzo1x_decompress_safe and a host batch
+    return the reference's code, length and bytes (tests/golden/longext.json,
+    from lib/minilzo.c: OUTPUT_OVERRUN -- a 32-bit sum wraps to a small length
+    and would decode the rest of the stream as valid)."""
+    import time
+    for c in longext:
+        t0 = time.perf_counter()
+        rc, out = lzo.lzo1x_decompress_safe(c["stream"], c["cap"])
+        dt = time.perf_counter() - t0
+        print(f"{c['kind']} zeros={c['zeros']}: rc={rc} out={len(out)} {dt * 1e3:.1f} ms")
+        assert (rc, len(out), hashlib.sha256(out).hexdigest()) == \
+            (c["rc"], c["out_len"], c["out_sha256"]), (c["kind"], c["zeros"])
+    sel = [c for c in longext if c["zeros"] == 16843009]
+    rc, status, outs = lzo.decompress_batch([c["stream"] for c in sel], [c["cap"] for c in sel])
+    assert rc == 0
+    for c, s, o in zip(sel, status, outs):
+        assert s == c["rc"], (c["kind"], s)
+
+
 def test_random_sizes_vs_oracle(dev, gu, oracle):
     rng = np.random.default_rng(5)
     blocks = [synth.block(int(rng.integers(0, 6)), 80000 + i, int(rng.integers(0, 140000)))
@@ -849,13 +886,15 @@ def test_latency_decoder_zero_runs_stay_linear(dev, oracle):
     cases = [(bytes(2 << 20), 1 << 20)]
     for d in (bytes(8 << 20), synth.block(synth.ITB, 71, 65536) + bytes(4 << 20) + synth.block(synth.ITB, 72, 65536)):
         cases.append((oracle.compress(d), len(d)))
+    lzo.lzo1x_decompress_safe(cases[1][0], cases[1][1])     # (warm: staging, code objects)
     for z, cap in cases:
         t0 = time.perf_counter()
         rc, out = lzo.lzo1x_decompress_safe(z, cap)
         dt = time.perf_counter() - t0
+        print(f"zero-run case: {len(z)} B in, rc={rc}, {dt * 1e3:.1f} ms")
         want = oracle.decompress_safe(z, cap)
         assert (rc, out) == want
-        assert dt < 1.0, dt
+        assert dt < 0.1, dt
 
 
 @pytest.mark.parametrize("k", [1, 3, 8])

@@ -56,6 +56,18 @@ def test_oracle_matches_unchecked_decoder(oracle, unchecked):
     assert {("valid", 0), ("trailing", -8), ("concat2", -8), ("eof_cut", -4)} <= kinds
 
 
+def test_oracle_long_extensions_past_32_bits(oracle, longext):
+    """A length extension whose 255-per-zero sum passes 2^32: the oracle keeps
+    the reference's 64-bit t (lib/minilzo.c:3805, :3862-3871, :3993-3998,
+    :4037-4042) and refuses it as the reference does."""
+    for c in longext:
+        s = c["stream"]
+        assert (len(s), hashlib.sha256(s).hexdigest()) == (c["stream_len"], c["stream_sha256"])
+        rc, out = oracle.decompress_safe(s, c["cap"])
+        assert (rc, len(out), hashlib.sha256(out).hexdigest()) == \
+            (c["rc"], c["out_len"], c["out_sha256"]), (c["kind"], c["zeros"])
+
+
 def test_oracle_pins_fwritev_columns(oracle, fwritev_columns):
     """The reference's hvfs_fwritev columns (api/api.c:6666-6680): the payload
     is the oracle's per-iovec streams back to back, and the reference's read
