@@ -28,6 +28,11 @@ size_t lzo_mi355x_worst_compress(size_t n);
 /* Number of usable GPUs (0 when none: every codec call then fails). */
 int lzo_mi355x_device_count(void);
 
+/* Re-read the POM_LZO_DEBUG environment variable (debug and experiment keys,
+ * INTEGRATION.md section 6).  The library reads it once, at the first use;
+ * a caller that changes it between calls (the tests) calls this after. */
+void lzo_mi355x_debug_reload(void);
+
 /* ---- device-resident batches ------------------------------------------------
  * All pointers are device (HBM) pointers; the call only enqueues work on
  * `stream` (a hipStream_t, NULL = default stream) and returns 0 or -1 on a

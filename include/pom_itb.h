@@ -88,8 +88,13 @@ int pom_abuf_close(struct pom_abuf *ab);
  * batch holding it is compressed, while the GPU compresses the next chunks.
  * locations[b] = the record's file offset (UINT64_MAX for a record with
  * err[b] == -EINVAL, which is not written).  Records are appended in the
- * order their chunks finish (largest first), not in index order.  Returns 0,
- * LZO_E_ERROR when the GPU path is unusable, or the first append's -errno. */
+ * order their chunks finish on the GPU, not in index order: two runs of the
+ * same batch can lay the file out differently (readers go by locations[];
+ * the debug key ooo=0 delivers chunks in launch order, largest blocks first).
+ * Returns 0, LZO_E_ERROR when the GPU path is unusable, or the first append's
+ * -errno; on any failure the append point is put back where it was on entry
+ * (nothing of the batch stays appended) and every locations[b] is UINT64_MAX,
+ * so the caller may retry the whole batch. */
 int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
                                       uint8_t **oi, int *err, size_t n, struct pom_abuf *ab,
                                       uint64_t *locations);
@@ -113,7 +118,8 @@ int pom_itb_read_batch(int fd, const uint64_t *locations, size_t n, uint8_t *con
  * -errno (-EINVAL: h.len < 264 or > cap[i]); derr[i] = the decoder's LZO_E_*
  * code (0 for an uncompressed record); len_ok[i] (may be NULL) as in
  * pom_itb_lzo_decompress_batch (1 for an uncompressed record); len[i] = the
- * record's h.len after decoding.  Returns 0, LZO_E_ERROR when the GPU path is
+ * record's h.len after decoding (0 when err[i] != 0: the buffer past the
+ * header is then undefined).  Returns 0, LZO_E_ERROR when the GPU path is
  * unusable, or LZO_E_OUT_OF_MEMORY. */
 int pom_itb_read_lzo_decompress_batch(int fd, const uint64_t *locations, size_t n, uint8_t *const *buf,
                                       const size_t *cap, size_t *len, int *err, int *derr, int *len_ok);

@@ -182,6 +182,27 @@ int pom_itb_lzo_compress_batch(uint8_t *const *in, uint8_t *const *tmp, const si
     return rc;
 }
 
+static int abuf_map(struct pom_abuf *ab);
+
+/* Puts the append point back to (file_offset, offset): the window holding it
+ * is mapped again if the appends moved on to later windows.  What was written
+ * past it is overwritten by the next appends and cut off at close. */
+static int abuf_rollback(struct pom_abuf *ab, uint64_t file_offset, size_t offset, uint64_t acclen)
+{
+    if (ab->file_offset != file_offset || !ab->addr) {
+        if (ab->addr && munmap(ab->addr, ab->win) != 0)
+            return -errno;
+        ab->addr = NULL;
+        ab->file_offset = file_offset;
+        const int rc = abuf_map(ab);
+        if (rc)
+            return rc;
+    }
+    ab->offset = offset;
+    ab->acclen = acclen;
+    return 0;
+}
+
 int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
                                       uint8_t **oi, int *err, size_t n, struct pom_abuf *ab,
                                       uint64_t *locations)
@@ -190,6 +211,10 @@ int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, c
         return LZO_E_OK;
     if (!ab || !ab->addr || !locations)
         return -EINVAL;
+    for (size_t b = 0; b < n; b++)
+        locations[b] = UINT64_MAX;
+    const uint64_t fo0 = ab->file_offset, acc0 = ab->acclen;
+    const size_t off0 = ab->offset;
     struct itb_wb w;
     int rc = itb_wb_init(&w, in, tmp, tmp_cap, oi, err, n);
     w.ab = ab;
@@ -199,6 +224,16 @@ int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, c
         rc = pom_compress_batch_chunked(w.src, w.slen, w.dst, w.dlen, w.st, n, itb_wb_chunk, &w);
     if (rc == LZO_E_OK && w.arc)
         rc = w.arc;
+    if (rc != LZO_E_OK) {
+        /* all or nothing: the chunks delivered before the failure were
+         * appended already; the append point goes back to where it was, so a
+         * retry of the batch writes every record once */
+        const int rb = abuf_rollback(ab, fo0, off0, acc0);
+        for (size_t b = 0; b < n; b++)
+            locations[b] = UINT64_MAX;
+        if (rb && rc == LZO_E_OK)
+            rc = rb;
+    }
     pthread_mutex_destroy(&w.mu);
     itb_wb_free(&w, n);
     return rc;
@@ -594,7 +629,6 @@ struct rd_dec {
     const size_t *plen;     /* per record */
     int *err;               /* per record */
     const size_t *comp;     /* batch block -> record */
-    size_t *tmp_ids;        /* scratch for a chunk's records */
     pthread_mutex_t mu;     /* (chunks of a multi-GPU batch on several threads) */
 };
 
@@ -679,7 +713,7 @@ int pom_itb_read_lzo_decompress_batch(int fd, const uint64_t *locations, size_t 
     }
     rc = LZO_E_OK;
     if (nc) {
-        struct rd_dec d = {fd, locations, buf, plen, err, comp, NULL, PTHREAD_MUTEX_INITIALIZER};
+        struct rd_dec d = {fd, locations, buf, plen, err, comp, PTHREAD_MUTEX_INITIALIZER};
         rc = pom_decompress_batch_chunked(src, slen, dst, dlen, st, nc, rd_dec_chunk, &d);
         pthread_mutex_destroy(&d.mu);
     }
@@ -688,8 +722,10 @@ int pom_itb_read_lzo_decompress_batch(int fd, const uint64_t *locations, size_t 
     /* 3. itb_lzo_decompress's header updates (mds/itb.c:2949-2980) */
     for (size_t i = 0; i < nc; i++) {
         const size_t b = comp[i];
-        if (err[b])                                 /* (the payload read failed) */
+        if (err[b]) {                               /* the payload read failed: the */
+            len[b] = 0;                             /* buffer past the header is undefined */
             continue;
+        }
         const uint32_t zlen = rd32(buf[b] + POM_ITBH_ZLEN_OFF);
         derr[b] = st[i];
         if (len_ok)

@@ -32,13 +32,35 @@
  * needs it; an unset key takes its default.  Keys: decoder=fast|win
  * (device batches), sc_copy=1, sc_combine=0, sc_lat=0, sc_lat_min=BYTES,
  * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, dec_small_first=0, ooo=0, enc_lds_max=N, enc_waves=1|2,
- * enc_grid=N.  Read at every use (tests change it between calls). */
+ * enc_grid=N, fail_chunk=K (tests: a device's K-th chunk delivery fails).  The variable is read once, at the first use, into a private
+ * copy; lzo_mi355x_debug_reload() reads it again (tests change it between
+ * calls).  So the hot paths never call getenv, and a concurrent setenv cannot
+ * race with a lookup. */
+static pthread_mutex_t dbg_mu = PTHREAD_MUTEX_INITIALIZER;
+static char dbg_val[512];
+static int dbg_loaded;
+
+void lzo_mi355x_debug_reload(void)
+{
+    pthread_mutex_lock(&dbg_mu);
+    const char *e = getenv("POM_LZO_DEBUG");
+    size_t n = e ? strlen(e) : 0;
+    if (n >= sizeof dbg_val)
+        n = sizeof dbg_val - 1;
+    memcpy(dbg_val, e ? e : "", n);
+    dbg_val[n] = 0;
+    __atomic_store_n(&dbg_loaded, 1, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&dbg_mu);
+}
+
 const char *pom_dbg_str(const char *key, char *buf, size_t n)
 {
-    const char *e = getenv("POM_LZO_DEBUG");
-    const size_t kl = strlen(key);
-    if (!e || !n)
+    if (!__atomic_load_n(&dbg_loaded, __ATOMIC_ACQUIRE))
+        lzo_mi355x_debug_reload();
+    const char *e = dbg_val;
+    if (!*e || !n)
         return NULL;
+    const size_t kl = strlen(key);
     for (const char *p = e; *p;) {
         const char *end = strchr(p, ',');
         const size_t len = end ? (size_t)(end - p) : strlen(p);
@@ -588,7 +610,7 @@ struct hbatch {
 };
 
 /* debug key host_timing=1: per-batch and per-chunk wall times on stderr (diagnostic) */
-static int g_timing = -1;
+#define g_timing (pom_dbg_int("host_timing", 0) == 1)
 
 static double now_ms(void)
 {
@@ -908,6 +930,10 @@ static int dev_run(void *arg, int d)
         struct layout L[kSlots];
         int live[kSlots] = {0};                /* slot holds a launched chunk */
         size_t from = 0;
+        /* (tests: debug key fail_chunk=K makes this device's K-th delivery fail
+         * as a failed GPU stream would) */
+        const long fail_at = pom_dbg_int("fail_chunk", -1);
+        long ndeliv = 0;
         for (int k = 0;; k++) {
             int cur = k % B->nslots;
             const int nxt = (k + 1) % B->nslots;
@@ -933,7 +959,8 @@ static int dev_run(void *arg, int d)
             }
             if (dj >= 0) {
                 const int ahead = !B->ooo && live[nxt] && nxt != dj;
-                if (chunk_deliver(&c->s[dj], &L[dj], B, ahead ? &c->s[nxt] : NULL, &L[nxt]) != 0) {
+                const int fail = fail_at >= 0 && ndeliv++ == fail_at;
+                if (fail || chunk_deliver(&c->s[dj], &L[dj], B, ahead ? &c->s[nxt] : NULL, &L[nxt]) != 0) {
                     rc = -1;
                     for (int j = 0; j < B->nslots; j++)
                         hipStreamSynchronize(c->s[j].stream);
@@ -1044,8 +1071,6 @@ static int batch_common_cb(enum op_kind kind, const uint8_t *const *src, const s
                            uint8_t *const *dst, size_t *dst_len, int *status, size_t nblocks,
                            pom_chunk_fn on_chunk, pom_chunk_fn pre_chunk, void *cb_ctx)
 {
-    if (g_timing < 0)
-        g_timing = pom_dbg_int("host_timing", 0) == 1;
     const double t0 = g_timing ? now_ms() : 0;
     struct tctx *t = tctx_get();
     if (!t)

@@ -41,7 +41,8 @@ LZO_VERSION = 0x2040
 EXPORTS = (
     "__lzo_init_v2", "lzo_version", "lzo_version_string", "lzo_version_date",
     "lzo1x_1_compress", "lzo1x_decompress", "lzo1x_decompress_safe",
-    "lzo_mi355x_worst_compress", "lzo_mi355x_device_count", "lzo_mi355x_decoded_length",
+    "lzo_mi355x_worst_compress", "lzo_mi355x_device_count", "lzo_mi355x_debug_reload",
+    "lzo_mi355x_decoded_length",
     "lzo_mi355x_compress_dev", "lzo_mi355x_decompress_dev",
     "lzo_mi355x_decompress_scratch", "lzo_mi355x_decompress_fallbacks", "lzo_mi355x_decoded_length_dev",
     "lzo_mi355x_compress_scratch",
@@ -64,6 +65,12 @@ _synth: Optional[ctypes.CDLL] = None
 _u8p = ctypes.c_void_p
 _ulong = ctypes.c_ulong
 _size = ctypes.c_size_t
+
+
+def debug_reload() -> None:
+    """Have the library re-read POM_LZO_DEBUG (it reads it once; see
+    include/lzo_mi355x.h lzo_mi355x_debug_reload)."""
+    load().lzo_mi355x_debug_reload()
 
 
 def load() -> ctypes.CDLL:

@@ -31,6 +31,17 @@ def _ensure_built():
 _ensure_built()
 
 
+@pytest.fixture(autouse=True)
+def _debug_keys_follow_env():
+    """The library reads POM_LZO_DEBUG once (lzo_host.c); tests that set it
+    (monkeypatch) get it re-read before and after them."""
+    from pomegranate_amd import lzo
+    lib = lzo.load()
+    lib.lzo_mi355x_debug_reload()
+    yield
+    lib.lzo_mi355x_debug_reload()
+
+
 class Oracle:
     """ctypes view of oracle/liboracle.so (the CPU restatement)."""
 

@@ -631,6 +631,7 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
     content models, sizes up to 300 KB, more blocks than one grid holds."""
     waves = "enc_waves=2" if kernel == "gdict_two_wave" else "enc_waves=1"
     monkeypatch.setenv("POM_LZO_DEBUG", waves)          # (lzo_host.c pom_dbg_str)
+    lzo.debug_reload()
     blocks = _sweep_blocks(300, 91)
     src = gu.device_batch(torch, blocks, dev, shift=1)
     dst = gu.empty_batch(torch, [lzo.worst_compress(len(b)) for b in blocks], dev, fill=0xA5)
@@ -643,6 +644,7 @@ def test_encoder_kernels_vs_oracle(dev, gu, oracle, kernel, monkeypatch):
         # taken through the block ticket (scratch sized for the batch, as the
         # ABI requires; its ticket word starts as garbage)
         monkeypatch.setenv("POM_LZO_DEBUG", waves + ",enc_grid=40")
+        lzo.debug_reload()
         scr = torch.full((lzo.compress_scratch_bytes(len(blocks)),), 0x5A, dtype=torch.uint8, device=dev)
         lzo.compress_dev(src, dst, olen, st, scratch=scr)
     torch.cuda.synchronize()

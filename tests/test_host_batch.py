@@ -43,6 +43,7 @@ def test_many_chunks_match_oracle(oracle, env):
     """A 1 MiB chunk budget cuts 300 mixed blocks into dozens of chunks; every
     block's output is still the oracle's, at its own destination."""
     env.setenv("POM_LZO_DEBUG", "chunk_mb=1")
+    lzo.debug_reload()
     env.setenv("POM_LZO_DEVICES", "0")
     rng = np.random.default_rng(4)
     sizes = [int(x) for x in rng.integers(0, 200000, 300)]

@@ -16,7 +16,7 @@ import struct
 import numpy as np
 import pytest
 
-from pomegranate_amd import itb, synth
+from pomegranate_amd import itb, lzo, synth
 
 
 def _records(n, seed=0, model=synth.ITB):
@@ -217,6 +217,7 @@ def test_compress_append_and_read_decompress_on_gpu(oracle, tmp_path, monkeypatc
         pytest.skip("no GPU")
     if chunk_mb:
         monkeypatch.setenv("POM_LZO_DEBUG", f"chunk_mb={chunk_mb}")
+        lzo.debug_reload()
     recs = _records(60, seed=21) + _records(3, seed=22, model=synth.RANDOM)
     bad = bytearray(itb.ITB_FULL)
     struct.pack_into("<I", bad, itb.LEN_OFF, 100)                 # h.len < 264: -EINVAL
@@ -264,3 +265,42 @@ def test_compress_append_and_read_decompress_on_gpu(oracle, tmp_path, monkeypatc
         h = bytearray(b[: itb.ITBH_SIZE])
         h[itb.ZLEN_OFF: itb.ZLEN_OFF + 4] = orig[itb.ZLEN_OFF: itb.ZLEN_OFF + 4]
         assert bytes(h) + bytes(b[itb.ITBH_SIZE: ln]) == orig
+
+
+@pytest.mark.gpu
+def test_append_batch_failure_leaves_the_file_as_it_was(tmp_path, monkeypatch):
+    """A failure partway through pom_itb_lzo_compress_append_batch (debug key
+    fail_chunk: the third chunk's delivery fails as a failed GPU stream would,
+    after earlier chunks were appended) puts the append point back: the call
+    fails, the file keeps only what was appended before it, and the same batch
+    retried lands once, after it."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    first = _records(5, seed=31)
+    recs = _records(50, seed=32)
+    tmps = [bytearray(itb.ITB_FULL) for _ in recs]
+    path = str(tmp_path / "fail.itb")
+    af = itb.AppendFile(path, win=1 << 20)                 # (windows cross: remaps too)
+    lead = af.append_batch(first, [itb.header_fields(r)[0] for r in first])
+    monkeypatch.setenv("POM_LZO_DEBUG", "chunk_mb=1,fail_chunk=2")
+    lzo.debug_reload()
+    with pytest.raises(RuntimeError):
+        itb.compress_append_batch(recs, tmps, af)
+    monkeypatch.setenv("POM_LZO_DEBUG", "chunk_mb=1")
+    lzo.debug_reload()
+    which, err, locs = itb.compress_append_batch(recs, tmps, af)
+    af.close()
+    assert err == [0] * len(recs)
+    sent = [t if w else r for r, t, w in zip(recs, tmps, which)]
+    lens = [itb.header_fields(o)[0] for o in sent]
+    lead_bytes = sum(itb.header_fields(r)[0] for r in first)
+    assert os.path.getsize(path) == lead_bytes + sum(lens)
+    assert min(locs) == lead_bytes
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        for loc, r in list(zip(lead, first)) + list(zip(locs, sent)):
+            ln = itb.header_fields(r)[0]
+            assert bytes(itb.read_record(fd, loc)[:ln]) == bytes(r[:ln])
+    finally:
+        os.close(fd)
