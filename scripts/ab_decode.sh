@@ -13,7 +13,7 @@ for spec in "$@"; do
   [ "$head" != "$name" ] && file=${head#*@}
   out=gpurun_out/variants/lib_$name.so
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C -Iinclude $flags -c $file -o /tmp/fast_$name.o || exit 1
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $C/lzo1x_kernels.o $C/lzo1x_encode_fast.o /tmp/fast_$name.o $C/lzo_host.o $C/batch_split.o $C/itb_codec.o $C/column_codec.o $C/xnet_frame.o -Wl,-Bsymbolic -lpthread || exit 1
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out /tmp/fast_$name.o $(ls $C/*.o | grep -v lzo1x_decode_fast.o) -Wl,-Bsymbolic -lpthread || exit 1
   for r in $(seq $REPS); do
     echo "== $name rep $r ($flags)"
     timeout -k 10 120 python scripts/diag_decode.py --lib $out --nostamps 2>&1 | grep -v amdgpu.ids || exit 1

@@ -13,7 +13,7 @@ for spec in "$@"; do
   [ "$head" != "$name" ] && file=${head#*@}
   out=gpurun_out/variants/libe_$name.so
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C -Iinclude $flags -c $file -o /tmp/encv_$name.o || exit 1
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out $C/lzo1x_kernels.o /tmp/encv_$name.o $C/lzo1x_decode_fast.o $C/lzo1x_decode_win.o $C/lzo1x_decode_ser.o $C/lzo_host.o $C/batch_split.o $C/itb_codec.o $C/column_codec.o $C/xnet_frame.o $C/io_util.o -Wl,-Bsymbolic -lpthread || exit 1
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $out /tmp/encv_$name.o $(ls $C/*.o | grep -v lzo1x_encode_fast.o) -Wl,-Bsymbolic -lpthread || exit 1
   for r in $(seq $REPS); do
     echo "== $name rep $r ($flags)"
     timeout -k 10 200 python scripts/diag_encode.py --lib $out --nostamps ${DIAGARGS:-} 2>&1 | grep -v amdgpu.ids || exit 1

@@ -1,5 +1,5 @@
 """Combined single calls: 8 threads of 64 KiB lzo1x_1_compress / lzo1x_decompress
-calls at once; run with POM_SC_TRACE=1 to see the group sizes the library forms."""
+calls at once; run with POM_LZO_DEBUG=sc_trace=1 to see the group sizes the library forms."""
 import ctypes
 import os
 import sys

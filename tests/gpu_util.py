@@ -96,17 +96,11 @@ def fetch(batch, olen, cap=None) -> List[bytes]:
 
 
 def gpu_decompress_win(torch, comps: Sequence[bytes], caps: Sequence[int], dev, kind: str = "win"):
-    """One throughput decoder alone, without the exact decoder behind it: the
-    windowed one (kind "win", lzo_mi355x_launch_decompress_win) or a rejected
-    one from scripts/experiments ("ser", "seg", "quad").  Returns the
-    outputs, statuses and the ids of the blocks it handed over (fallback list)."""
+    """The windowed decoder alone (lzo_mi355x_launch_decompress_win), without
+    the exact decoder behind it.  Returns the outputs, statuses and the ids of
+    the blocks it handed over (fallback list)."""
     import ctypes
-    import os
     lib = lzo.load()
-    if not hasattr(lib, f"lzo_mi355x_launch_decompress_{kind}"):
-        # a rejected decoder kept for A/B runs (scripts/experiments, built there)
-        here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        lib = ctypes.CDLL(os.path.join(here, "scripts", "experiments", f"libdecode_{kind}.so"))
     fn = getattr(lib, f"lzo_mi355x_launch_decompress_{kind}")
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p] * 10 + [ctypes.c_uint32, ctypes.c_void_p]

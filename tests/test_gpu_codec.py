@@ -741,8 +741,8 @@ def test_encoder_block_tickets_mixed_sizes(dev, gu):
 
 @pytest.mark.parametrize("kind", ["win"])
 def test_window_decoder_every_valid_stream(dev, gu, kind):
-    """The windowed (lzo1x_decode_win.hip) and table-walk
-    (lzo1x_decode_ser.hip) decoders alone, without the exact decoder behind it: every content model (incompressible blocks with
+    """The windowed decoder (lzo1x_decode_win.hip) alone, without the exact
+    decoder behind it: every content model (incompressible blocks with
     literal runs far longer than a 2 KiB piece, all-zero blocks with length
     extensions past a piece), ITB blocks over the C4/C5 size range, the
     adversarial blocks and a 1 MiB block (the 64 KiB LDS ring wraps 16 times)
