@@ -251,10 +251,35 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 constexpr int kCmpW = POM_ENC_CMP;
 constexpr uint32_t kCmpB = 4 * kCmpW;            // match bytes known without an extension
 
+// Bits [off, off + width) of a 64-bit mask, width < 64 (one s_bfm_b64:
+// ((1 << width) - 1) << off; the compiler's form takes four instructions).
+__device__ __forceinline__ uint64_t bit_range(uint32_t off, uint32_t width)
+{
+    uint64_t m;
+    asm("s_bfm_b64 %0, %1, %2" : "=s"(m) : "s"(width), "s"(off));
+    return m;
+}
+
 // Index of the first differing byte of two NW-dword strings (4 * NW: none).
+// v_ffbl_b32 of 0 is 0xFFFFFFFF, which a saturating add of 32i keeps, so the
+// minimum over the dwords of ffbl + 32i is the first differing bit: xor,
+// ffbl, add and a min3 half of the time per dword, no compare or select.
+#ifndef POM_ENC_FD
+#define POM_ENC_FD 1
+#endif
 template <int NW>
 __device__ __forceinline__ uint32_t first_diff(const uint32_t (&a)[NW], const uint32_t (&b)[NW])
 {
+#if POM_ENC_FD
+    uint32_t m = 32 * NW;                           // (bit index of the first difference)
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        uint32_t f;                                  // (asm: the compiler rebuilds selects from ctz)
+        asm("v_ffbl_b32 %0, %1" : "=v"(f) : "v"(a[i] ^ b[i]));           // 0xFFFFFFFF: equal
+        m = min(m, __builtin_elementwise_add_sat(f, 32u * i));          // (saturates: equal stays max)
+    }
+    return m >> 3;
+#else
     uint32_t m = 4 * NW;
 #pragma unroll
     for (int i = NW - 1; i >= 0; i--) {
@@ -262,6 +287,7 @@ __device__ __forceinline__ uint32_t first_diff(const uint32_t (&a)[NW], const ui
         m = x ? 4u * i + ((uint32_t)__builtin_ctz(x) >> 3) : m;
     }
     return m;
+#endif
 }
 
 // Match length from index k0 on (the first k0 bytes match), wave-parallel,
@@ -557,6 +583,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
         uint32_t ip = 4;
         uint32_t base = 0;                          // dictionary position base
         uint32_t wtag = 0xFFFFFEu;                  // claim tag of the window (one per window, > 0)
+        uint32_t prio_ip = 0;                       // (FUSED priority) next ip at which it steps down
         // Probe words of the window (position ip + l): the next window's are
         // read as soon as its start is known, ahead of the token and
         // dictionary writes.
@@ -567,10 +594,11 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             if (STAMPS)
                 acc[EC_WINDOWS] += 1;
 #if POM_ENC_PRIO
-            if (FUSED && E->prio) {
-                // (one-wave kernel, one block per workgroup) blocks that are behind
-                // (more input left) get the issue slots first, so the workgroups of
-                // a CU finish together
+            // (one-wave kernel, one block per workgroup) blocks that are behind
+            // (more input left) get the issue slots first, so the workgroups of
+            // a CU finish together.  The priority steps down at most three
+            // times a block: it is set again only once ip passes prio_ip.
+            if (FUSED && E->prio && ip >= prio_ip) {
                 const uint32_t left = n - ip, st = POM_ENC_PRIO_STEP;
                 const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
                                                                   : left >= st ? 1u : 0u);
@@ -580,6 +608,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 case 1: __builtin_amdgcn_s_setprio(1); break;
                 default: __builtin_amdgcn_s_setprio(0); break;
                 }
+                prio_ip = q ? n - q * st + 1 : 0xFFFFFFFFu;     // left < q * st from there on
             }
 #endif
             if (ip + kWave - base >= 0xFFFFu) {     // this window's positions would not fit
@@ -664,22 +693,25 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             uint64_t path = 0, mstart = 0;
             uint32_t end = 0;                        // lane where the path leaves the window
             uint32_t nmatch = 0;
-            // the path from lane `from` on (lanes below it stay as they are)
+            // The path from lane `from` on (lanes below it stay as they are):
+            // from `end`, the next match lane q -- the literal lanes end .. q-1
+            // before it -- then on from q + its length.
             auto walk = [&](uint32_t from) {
                 end = from;
-                while (end < nact) {
+#pragma unroll
+                for (int it = 0; it < POM_ENC_PATHMAX; it++) {
+                    if (end >= nact || nmatch >= POM_ENC_PATHMAX)
+                        break;
                     if (STAMPS)
                         acc[EC_PATHIT] += 1;
-                    const uint64_t rest = okm & (~0ull << end);
-                    const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
-                    const uint32_t lit_end = q < nact ? q : nact;
-                    if (lit_end > end)               // literal lanes end .. lit_end-1
-                        path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
-                    if (q >= nact) {
+                    const uint64_t rest = okm & (~0ull << end);     // (end < 64 here)
+                    if (!rest) {                     // literal lanes to the last active one
+                        path |= nact - end >= 64 ? ~0ull : bit_range(end, nact - end);
                         end = nact;
                         break;
                     }
-                    path |= 1ull << q;
+                    const uint32_t q = (uint32_t)__builtin_ctzll(rest);   // (< nact: ok lanes are active)
+                    path |= bit_range(end, q - end) | (1ull << q);        // (q - end < 64)
                     mstart |= 1ull << q;
                     uint32_t len = lane_read(mlen, q);
                     if (len == kCmpB && n - (ip + q) > kCmpB) {
@@ -691,8 +723,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                         mlen = l == q ? len : mlen;
                     }
                     end = q + len;
-                    if (++nmatch >= POM_ENC_PATHMAX) // the window ends after this match
-                        break;
+                    nmatch++;                        // (the window ends after the last one)
                 }
             };
             walk(0);
@@ -703,13 +734,16 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // table keeps, per hashed slot, the lowest lane of this window
             // writing it (ds_min of tag|lane; a wave's LDS operations complete
             // in order, so the reads below see every post).  A path lane is
-            // inexact only if a lower path lane writes a slot it read.  The
-            // first such lane c is decided again: its entry is the position of
-            // the last lower path lane j writing that slot -- less than 64
+            // inexact only if a lower path lane writes a slot it read.  Such a
+            // lane c, lowest first, is decided again: its entry is the position
+            // of the last lower path lane j writing that slot -- less than 64
             // back, so the candidate passes the M2_MAX_OFFSET test -- and j's
-            // probe words are the candidate's bytes.  The path is walked again
-            // from c and the claims re-posted under a new tag; after
-            // POM_ENC_FWD such rounds the window ends at the next such lane.
+            // probe words are the candidate's bytes.  When the new decision
+            // leaves c's kind, length and written slot as they were (the path
+            // and the claims stand), the round goes on to the next conflicting
+            // lane; otherwise the path is walked again from c and the claims
+            // re-posted under a new tag.  After POM_ENC_FWD rounds the window
+            // ends at the next conflicting lane.
             uint64_t resolved = 0, superseded = 0;   // (superseded: a later lane writes its slot)
             uint64_t um2 = wave_ballot(use2);        // lanes that read the secondary slot
             for (uint32_t round = 0;; round++) {
@@ -723,46 +757,64 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 // this window writes (h1, or h2 when use2)
                 const uint64_t cf1 = mask_eq(t1 >> 8, wtag) & mask_lt(t1 & 0xFFu, l);
                 const uint64_t cf2 = um2 & mask_eq(t2 >> 8, wtag) & mask_lt(t2 & 0xFFu, l);
-                const uint64_t cm = path & ~resolved & (cf1 | cf2);
+                uint64_t cm = path & ~resolved & (cf1 | cf2);
                 wtag--;
                 if (!cm)
                     break;
-                const uint32_t c = (uint32_t)__builtin_ctzll(cm);   // never lane 0
                 if (round >= POM_ENC_FWD) {
-                    end = c;                         // the window ends at a path lane
+                    end = (uint32_t)__builtin_ctzll(cm);   // the window ends at a path lane
                     break;
                 }
-                if (STAMPS)
-                    acc[EC_FWD] += 1;
-                resolved |= 1ull << c;
-                const uint64_t below_c = (1ull << c) - 1;
-                const uint64_t pm = path & below_c;  // exact path lanes below c
-                const uint32_t h1c = lane_read(h1, c), h2c = lane_read(h2, c);
-                const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
-                const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (((um2 >> c) & 1ull) ? ~0ull : 0ull);
-                if (!wm1 && !wm2)
-                    continue;                        // a claim-table alias: c was exact
-                const bool via2 = wm1 == 0;          // h1 unchanged, its test failed again: h2
-                const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
-                superseded |= 1ull << j;             // c writes j's slot after j
-                uint32_t pj[kCmpW];
+                bool moved = false;                  // the path changed: claims again
+                while (cm) {
+                    const uint32_t c = (uint32_t)__builtin_ctzll(cm);   // never lane 0
+                    cm &= cm - 1;
+                    if (STAMPS)
+                        acc[EC_FWD] += 1;
+                    resolved |= 1ull << c;
+                    const uint64_t below_c = (1ull << c) - 1;
+                    const uint64_t pm = path & below_c;  // exact path lanes below c
+                    const uint32_t h1c = lane_read(h1, c), h2c = lane_read(h2, c);
+                    const bool u2c = ((um2 >> c) & 1ull) != 0;
+                    const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
+                    const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (u2c ? ~0ull : 0ull);
+                    if (!wm1 && !wm2)
+                        continue;                    // a claim-table alias: c was exact
+                    const bool via2 = wm1 == 0;      // h1 unchanged, its test failed again: h2
+                    const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
+                    superseded |= 1ull << j;         // c writes j's slot after j
+                    uint32_t pj[kCmpW];
 #pragma unroll
-                for (int i = 0; i < kCmpW; i++)
-                    pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)pw[i]);
-                uint32_t mc = first_diff<kCmpW>(pj, pw);
-                mc = mc < n - p ? mc : n - p;
-                const bool isc = l == c;
-                ok = isc ? ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0 : ok;
-                mlen = isc ? mc : mlen;
-                cand = isc ? ip + j : cand;
-                slot = isc ? (via2 ? h2 : h1) : slot;
-                use2 = isc ? via2 : use2;
-                um2 = via2 ? um2 | (1ull << c) : um2 & ~(1ull << c);
-                okm = wave_ballot(ok);
-                path &= below_c;
-                mstart &= below_c;
-                nmatch = (uint32_t)__builtin_popcountll(mstart);
-                walk(c);
+                    for (int i = 0; i < kCmpW; i++)
+                        pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)pw[i]);
+                    uint32_t mc = first_diff<kCmpW>(pj, pw);
+                    mc = mc < n - p ? mc : n - p;
+                    const bool isc = l == c;
+                    const bool nok = ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0;
+                    const bool ook = ((okm >> c) & 1ull) != 0;
+                    const uint64_t nokm = wave_ballot(isc ? nok : ok);
+                    const uint32_t omc = lane_read(mlen, c), nmc = lane_read(mc, c);
+                    // the same kind, length (not one an extension decides) and slot
+                    const bool same = ((nokm >> c) & 1ull) == ook && via2 == u2c &&
+                                      (!ook || (nmc == omc && omc < kCmpB));
+                    ok = isc ? nok : ok;
+                    mlen = isc ? mc : mlen;
+                    cand = isc ? ip + j : cand;
+                    slot = isc ? (via2 ? h2 : h1) : slot;
+                    use2 = isc ? via2 : use2;
+                    um2 = via2 ? um2 | (1ull << c) : um2 & ~(1ull << c);
+                    okm = nokm;
+                    if (same)
+                        continue;                    // path and claims stand: the next conflict
+                    path &= below_c;
+                    mstart &= below_c;
+                    nmatch = (uint32_t)__builtin_popcountll(mstart);
+                    walk(c);
+                    moved = true;
+                    break;
+                }
+                if (!moved)
+                    break;                           // every conflict resolved in place: exact
             }
             if (STAMPS) {                            // (why the window ended)
                 acc[EC_C2NEED] += end > 64 ? 1 : 0;  // a match crossing its last lane
