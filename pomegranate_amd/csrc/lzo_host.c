@@ -1233,7 +1233,7 @@ struct sc_queue {
 };
 
 static struct sc_queue sc_q[kMaxDev];
-static __thread uint64_t sc_last_group;      /* group of this thread's last single call */
+static __thread uint64_t sc_last_group[kMaxDev];   /* per device: group of this thread's last single call */
 static pthread_once_t sc_once = PTHREAD_ONCE_INIT;
 
 static void sc_init(void)
@@ -1508,7 +1508,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
          * them ~50 us to queue.  (A thread that was not in it -- a lone caller
          * after a burst of others -- does not wait: ADVICE round 3.) */
         q->leader = 1;
-        if (q->last_k > 1 && q->head == q->tail && sc_last_group == q->seq) {
+        if (q->last_k > 1 && q->head == q->tail && sc_last_group[dev] == q->seq) {
             struct timespec ts;
             clock_gettime(CLOCK_MONOTONIC, &ts);
             ts.tv_nsec += 50000;
@@ -1551,7 +1551,7 @@ static int single_call(enum sc_kind kind, const uint8_t *src, size_t src_len, ui
         pthread_cond_broadcast(&q->cv);
     }
     pthread_mutex_unlock(&q->mu);
-    sc_last_group = r.group;
+    sc_last_group[dev] = r.group;
     *produced = r.produced;
     return r.rc;
 }

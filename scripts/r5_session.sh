@@ -17,7 +17,7 @@ step() {
 }
 python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { echo build failed; tail "$OUT/build.log"; exit 1; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  step pytest_gpu 420 python -u -m pytest tests -v -s -m gpu -x --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+  step pytest_gpu 420 python -u -m pytest tests -v -s -m gpu ${PYTEST_X:--x} --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 fi
 # (A/B libraries: built beforehand with scripts/ab_build.sh, they travel in-tree)
 for r in 1 2 3; do
