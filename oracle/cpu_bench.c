@@ -6,12 +6,13 @@
  * the reference was not built, the oracle port (oracle/liboracle.so) -- on a
  * fixed number of host threads with no Python in the loop:
  *
- *   cpu_bench LIB SAMPLE THREADS SECONDS
+ *   cpu_bench LIB SAMPLE THREADS SECONDS [PIN]
  *
  * SAMPLE holds the blocks: u32 count, then per block u32 n, u32 z, n plain
  * bytes, z compressed bytes (bench.py writes it from the GPU's own batch).
- * Each thread is pinned to one CPU of the process's affinity set (thread t to
- * its t-th CPU, wrapping), owns its wrkmem and buffers, and takes the blocks
+ * Each thread is pinned to one CPU of the process's affinity set (PIN "1",
+ * the default: thread t to its t-th CPU, wrapping; "spread": CPU t * (set /
+ * THREADS); "0": not pinned), owns its wrkmem and buffers, and takes the blocks
  * t, t + THREADS, ... round robin.  Phase 1 decompresses (lzo1x_decompress,
  * the unchecked decoder Pomegranate's callers use: mds/itb.c:2964,
  * mdsl/gc.c:770) for 0.6 * SECONDS, phase 2 compresses (lzo1x_1_compress,
@@ -155,7 +156,7 @@ static uint8_t *slurp(const char *path, size_t *len)
 int main(int argc, char **argv)
 {
     if (argc < 5) {
-        fprintf(stderr, "usage: %s LIB SAMPLE THREADS SECONDS\n", argv[0]);
+        fprintf(stderr, "usage: %s LIB SAMPLE THREADS SECONDS [PIN: 1|0|spread]\n", argv[0]);
         return 2;
     }
     void *lib = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
@@ -228,18 +229,26 @@ int main(int argc, char **argv)
     free(out);
     free(wrk);
 
+    /* PIN: "1" (default) thread t on the t-th CPU of the affinity set, "0" no
+     * pinning (the scheduler places the threads), "spread" thread t on CPU
+     * t * (affinity set / threads) of the set */
+    const char *pin = argc > 5 ? argv[5] : "1";
     cpu_set_t aff;
     int cpus[CPU_SETSIZE], naff = 0;
     if (sched_getaffinity(0, sizeof(aff), &aff) == 0)
         for (int c = 0; c < CPU_SETSIZE; c++)
             if (CPU_ISSET(c, &aff))
                 cpus[naff++] = c;
+    const int nthr_arg = atoi(argv[3]) > 0 ? atoi(argv[3]) : 1;
+    const int stride = strcmp(pin, "spread") == 0 && naff > nthr_arg ? naff / nthr_arg : 1;
+    if (strcmp(pin, "0") == 0)
+        naff = 0;
     struct thr *T = calloc((size_t)nthreads, sizeof(*T));
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
     for (int i = 0; i < nthreads; i++) {
         T[i].index = i;
-        T[i].cpu = naff ? cpus[i % naff] : -1;
+        T[i].cpu = naff ? cpus[(i * stride) % naff] : -1;
         T[i].dec_s = 0.6 * secs;
         T[i].comp_s = 0.4 * secs;
         T[i].bar = &bar;
@@ -255,11 +264,11 @@ int main(int argc, char **argv)
         ct = T[i].comp_time > ct ? T[i].comp_time : ct;
         errors += T[i].errors;
     }
-    printf("{\"kind\": \"%s\", \"threads\": %d, \"affinity_cpus\": %d, \"blocks\": %u, "
+    printf("{\"kind\": \"%s\", \"threads\": %d, \"affinity_cpus\": %d, \"pin\": \"%s\", \"blocks\": %u, "
            "\"decompress_Bps\": %.1f, \"compress_Bps\": %.1f, \"decompress_s\": %.3f, "
            "\"compress_s\": %.3f, \"byte_identical\": %u, \"decoded\": %u, \"errors\": %d, "
            "\"per_thread_decompress_Bps\": [",
-           is_ref ? "reference" : "port", nthreads, naff, nblocks, dt > 0 ? db / dt : 0.0,
+           is_ref ? "reference" : "port", nthreads, naff, pin, nblocks, dt > 0 ? db / dt : 0.0,
            ct > 0 ? cb / ct : 0.0, dt, ct, identical, decoded, errors);
     for (int i = 0; i < nthreads; i++)
         printf("%s%.1f", i ? ", " : "", T[i].dec_time > 0 ? T[i].dec_bytes / T[i].dec_time : 0.0);

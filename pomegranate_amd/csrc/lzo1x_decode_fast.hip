@@ -553,6 +553,21 @@ __device__ __forceinline__ void lds_write1(uint32_t a, uint32_t v)
 #ifndef POM_DEC_R5
 #define POM_DEC_R5 1                             // round-5 step: no exec-masked branches in the byte moving
 #endif
+#ifndef POM_DEC_R5_BASE
+#define POM_DEC_R5_BASE POM_DEC_R5               // LDS bases from one readfirstlane
+#endif
+#ifndef POM_DEC_R5_TAG
+#define POM_DEC_R5_TAG POM_DEC_R5                // chunk tags written without a branch
+#endif
+#ifndef POM_DEC_R5_MOD
+#define POM_DEC_R5_MOD POM_DEC_R5                // period reduction without a branch
+#endif
+#ifndef POM_DEC_R5_MERGE
+#define POM_DEC_R5_MERGE POM_DEC_R5              // two-read merge masks without branches
+#endif
+#ifndef POM_DEC_R5_WRITE
+#define POM_DEC_R5_WRITE POM_DEC_R5              // partial-chunk writes to a trash slot
+#endif
 // The first len (<= 16) bytes of v at LDS address a, without exec branches:
 // every piece (b128 for a whole chunk, else b64/b32/b16/b8) is written by
 // every lane, at a, or at the trash slot t when the lane's chunk does not
@@ -1452,7 +1467,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     }
 
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-#if POM_DEC_R5
+#if POM_DEC_R5_BASE
     // (LDS addresses as offsets from one readfirstlane'd base: the compiler
     // otherwise re-derives each generic-to-LDS cast, with its null check, in
     // every step)
@@ -1463,6 +1478,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
 #else
     const uint32_t base = lds_off(&S);
     const uint32_t psel0 = lds_off(&S.psel[0][0][0]), psel1 = lds_off(&S.psel[1][0][0]);
+    const uint32_t trash = lds_off(&S.trash[0]);
 #endif
     uint32_t carry = 0;                        // output produced so far
     uint32_t issued_seen = 0, landed_seen = 0; // last `issued` / `landed` read
@@ -1645,7 +1661,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     // before chunk C + l (a ballot and mbcnt, no scan).
                     tag++;
                     const uint32_t tagv = tag | 0x80000000u;   // src_issue's byte flags never set bit 31
-#if POM_DEC_R5
+#if POM_DEC_R5_TAG
                     S.flags[starter && cs >= C && cs < C + kWave ? cs - C : (uint32_t)kWave] = tagv;
 #else
                     if (starter && cs >= C && cs < C + kWave)
@@ -1698,7 +1714,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     const bool lin = (op.y & kLitFlag) != 0;
                     const uint32_t bb = op.y & ~kLitFlag;
                     uint32_t r0 = k16;
-#if POM_DEC_R5
+#if POM_DEC_R5_MOD
                     // (p == 0: the inverse is 0, so r0 stays k16 without a branch)
                     r0 = k16 - p * (uint32_t)__umulhi(k16, pr.y);
                     r0 = min(r0, r0 - p);
@@ -1760,7 +1776,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     if (any_two) {
                         // bytes i < n1 from vA, the rest from vB
                         const uint32_t n = two ? n1 : 16u;
-#if POM_DEC_R5
+#if POM_DEC_R5_MERGE
                         // bytes below n (1 <= n <= 16) as two 64-bit masks, no
                         // branches: (2 << (8k - 1)) - 1 is k bytes for k = 1..8
                         const uint32_t nl = n < 8u ? n : 8u, nh = n > 8u ? n - 8u : 1u;
@@ -1790,7 +1806,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     // ---- destination: the ring at x -----------------------------
                     const uint32_t xd = x & kRingMask;
                     const bool wcross = live && xd + len > kRing;
-#if POM_DEC_R5
+#if POM_DEC_R5_WRITE
                     const uint32_t wlen = live && !wcross ? len : 0u;
                     lds_write_part_bf(base + xd, v, wlen, trash);
                     if (mask_lt(xd, 16u) & mask_lt(0u, wlen))   // keep the mirror of ring[0, 16)

@@ -115,6 +115,15 @@ static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budge
 #ifndef POM_ENC_PRIO
 #define POM_ENC_PRIO 1                          // one-wave kernel: wave priority by input bytes left
 #endif
+#ifndef POM_ENC_LAZYPRIO
+#define POM_ENC_LAZYPRIO 1                      // set the priority only when it steps down
+#endif
+#ifndef POM_ENC_WALK2
+#define POM_ENC_WALK2 1                         // path walk: unrolled, literal ranges by s_bfm_b64
+#endif
+#ifndef POM_ENC_SAME
+#define POM_ENC_SAME 1                          // conflicts that keep the path resolved in place
+#endif
 #ifndef POM_ENC_PRIO_STEP
 #define POM_ENC_PRIO_STEP 8192
 #endif
@@ -598,7 +607,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // (more input left) get the issue slots first, so the workgroups of
             // a CU finish together.  The priority steps down at most three
             // times a block: it is set again only once ip passes prio_ip.
-            if (FUSED && E->prio && ip >= prio_ip) {
+            if (FUSED && E->prio && (!POM_ENC_LAZYPRIO || ip >= prio_ip)) {
                 const uint32_t left = n - ip, st = POM_ENC_PRIO_STEP;
                 const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
                                                                   : left >= st ? 1u : 0u);
@@ -696,6 +705,38 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // The path from lane `from` on (lanes below it stay as they are):
             // from `end`, the next match lane q -- the literal lanes end .. q-1
             // before it -- then on from q + its length.
+#if !POM_ENC_WALK2
+            auto walk = [&](uint32_t from) {
+                end = from;
+                while (end < nact) {
+                    if (STAMPS)
+                        acc[EC_PATHIT] += 1;
+                    const uint64_t rest = okm & (~0ull << end);
+                    const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
+                    const uint32_t lit_end = q < nact ? q : nact;
+                    if (lit_end > end)               // literal lanes end .. lit_end-1
+                        path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
+                    if (q >= nact) {
+                        end = nact;
+                        break;
+                    }
+                    path |= 1ull << q;
+                    mstart |= 1ull << q;
+                    uint32_t len = lane_read(mlen, q);
+                    if (len == kCmpB && n - (ip + q) > kCmpB) {
+                        if (STAMPS)
+                            acc[EC_EXTEND] += 1;
+                        len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
+                        if (STAMPS)
+                            acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
+                        mlen = l == q ? len : mlen;
+                    }
+                    end = q + len;
+                    if (++nmatch >= POM_ENC_PATHMAX) // the window ends after this match
+                        break;
+                }
+            };
+#else
             auto walk = [&](uint32_t from) {
                 end = from;
 #pragma unroll
@@ -726,6 +767,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                     nmatch++;                        // (the window ends after the last one)
                 }
             };
+#endif
             walk(0);
 
             ESTAMP(EP_PATH);
@@ -778,8 +820,12 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                     const bool u2c = ((um2 >> c) & 1ull) != 0;
                     const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
                     const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (u2c ? ~0ull : 0ull);
-                    if (!wm1 && !wm2)
-                        continue;                    // a claim-table alias: c was exact
+                    if (!wm1 && !wm2) {              // a claim-table alias: c was exact
+                        if (POM_ENC_SAME)
+                            continue;
+                        moved = true;                // (the old protocol: claims again)
+                        break;
+                    }
                     const bool via2 = wm1 == 0;      // h1 unchanged, its test failed again: h2
                     const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
                     superseded |= 1ull << j;         // c writes j's slot after j
@@ -804,7 +850,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                     use2 = isc ? via2 : use2;
                     um2 = via2 ? um2 | (1ull << c) : um2 & ~(1ull << c);
                     okm = nokm;
-                    if (same)
+                    if (POM_ENC_SAME && same)
                         continue;                    // path and claims stand: the next conflict
                     path &= below_c;
                     mstart &= below_c;

@@ -7,7 +7,7 @@ set -eu
 name=$1; shift
 C=pomegranate_amd/csrc
 enc=$C/lzo1x_encode_fast.hip; dec=$C/lzo1x_decode_fast.hip; encflags=""; decflags=""
-for kv in "$@"; do eval "$kv"; done
+for kv in "$@"; do declare -- "$kv"; done
 mkdir -p scripts/ab
 HIPCC="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$C -Iinclude"
 $HIPCC $encflags -c $enc -o /tmp/ab_enc_$name.o
