@@ -566,13 +566,13 @@ __device__ __forceinline__ void lds_write1(uint32_t a, uint32_t v)
 #define POM_DEC_R5_MERGE POM_DEC_R5              // two-read merge masks without branches
 #endif
 #ifndef POM_DEC_R5_WRITE
-#define POM_DEC_R5_WRITE POM_DEC_R5              // partial-chunk writes to a trash slot
+#define POM_DEC_R5_WRITE 0                       // partial-chunk writes to a trash slot (A/B r05a: 4% slower)
 #endif
 // The first len (<= 16) bytes of v at LDS address a, without exec branches:
 // every piece (b128 for a whole chunk, else b64/b32/b16/b8) is written by
 // every lane, at a, or at the trash slot t when the lane's chunk does not
 // take it; a piece no lane takes is skipped by a uniform branch.
-__device__ __forceinline__ void lds_write_part_bf(uint32_t a, uint4 v, uint32_t len, uint32_t t)
+__device__ __forceinline__ __attribute__((unused)) void lds_write_part_bf(uint32_t a, uint4 v, uint32_t len, uint32_t t)
 {
     const bool f16 = len == 16u, f8 = (len & 8u) != 0, f4 = (len & 4u) != 0, f2 = (len & 2u) != 0,
                f1 = (len & 1u) != 0;
@@ -1474,11 +1474,11 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_off(&S));
     const uint32_t psel0 = base + (uint32_t)offsetof(FastLds, psel);
     const uint32_t psel1 = psel0 + (uint32_t)sizeof(S.psel[0]);
-    const uint32_t trash = base + (uint32_t)offsetof(FastLds, trash);
+    [[maybe_unused]] const uint32_t trash = base + (uint32_t)offsetof(FastLds, trash);
 #else
     const uint32_t base = lds_off(&S);
     const uint32_t psel0 = lds_off(&S.psel[0][0][0]), psel1 = lds_off(&S.psel[1][0][0]);
-    const uint32_t trash = lds_off(&S.trash[0]);
+    [[maybe_unused]] const uint32_t trash = lds_off(&S.trash[0]);
 #endif
     uint32_t carry = 0;                        // output produced so far
     uint32_t issued_seen = 0, landed_seen = 0; // last `issued` / `landed` read

@@ -122,7 +122,10 @@ static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budge
 #define POM_ENC_WALK2 1                         // path walk: unrolled, literal ranges by s_bfm_b64
 #endif
 #ifndef POM_ENC_SAME
-#define POM_ENC_SAME 1                          // conflicts that keep the path resolved in place
+#define POM_ENC_SAME 0                          // conflicts that keep the path resolved in place (A/B r05a: 3.8% slower on C3)
+#endif
+#ifndef POM_ENC_DPF
+#define POM_ENC_DPF 1                           // prefetch the next window's dictionary lines into L2
 #endif
 #ifndef POM_ENC_PRIO_STEP
 #define POM_ENC_PRIO_STEP 8192
@@ -547,6 +550,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
     const uintptr_t pf_lines = (uintptr_t)in & ~(uintptr_t)127;
     const uintptr_t pf_last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
     uint32_t pf = 0, pf_acc = 0, pf_new = 0;
+    uint32_t dpf1 = 0, dpf2 = 0;                    // (POM_ENC_DPF) the next window's dictionary lines
     auto prefetch = [&](uint32_t at) {
         pf_acc ^= pf_new;
         pf_new = 0;
@@ -648,6 +652,8 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                                                    (pw[0] >> 16) & 0xFF, pw[0] >> 24);
             const uint32_t h2 = emit::slot_secondary(h1);
             const uint32_t e1 = D.get(h1), e2 = D.get(h2);
+            if (POM_ENC_DPF && GD && FUSED)
+                pf_new ^= dpf1 ^ dpf2;               // (their wait merges with the probes')
             const uint32_t w1 = active && e1 ? base + e1 - 1 : 0u;   // (positions >= 4: 0 stays "empty")
             const uint32_t w2 = active && e2 ? base + e2 - 1 : 0u;
             const uint64_t am = mask_lt(p, ip_end) | 1ull;      // (active)
@@ -769,6 +775,13 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             };
 #endif
             walk(0);
+            // The next window's probe words, issued now (read again below when
+            // forwarding moves the window's end): after the claims, their
+            // hashes pull the next window's dictionary lines into L2.
+            uint32_t npw[kCmpW];
+            uint32_t npw_end = end;
+            if (POM_ENC_DPF && GD && FUSED)
+                load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
 
             ESTAMP(EP_PATH);
             // ---- exactness: claims among the path lanes, and forwarding ------
@@ -868,8 +881,15 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
 
-            uint32_t npw[kCmpW];
-            load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
+            if (!(POM_ENC_DPF && GD && FUSED) || end != npw_end)
+                load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
+            npw_end = end;
+            if (POM_ENC_DPF && GD && FUSED) {
+                const uint32_t nh1 = emit::slot_primary(npw[0] & 0xFF, (npw[0] >> 8) & 0xFF,
+                                                        (npw[0] >> 16) & 0xFF, npw[0] >> 24);
+                dpf1 = D.get(nh1);                   // (line prefetch: the values are not used)
+                dpf2 = D.get(emit::slot_secondary(nh1));
+            }
 
             ESTAMP(EP_CLAIM);
             // ---- tokens for the matches before the cut ------------------------

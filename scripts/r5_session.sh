@@ -26,6 +26,7 @@ for r in 1 2 3; do
   done
   [ -n "${AB:-}" ] && step ab_cur_$r 120 python scripts/ab_kernels.py --reps 10
 done
+[ -n "${EXTRA:-}" ] && step extra 300 $EXTRA
 [ "${SKIP_SMOKE:-0}" != 1 ] && step smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
 [ "${SKIP_BENCH:-0}" != 1 ] && step bench 420 python bench.py ${BENCH_ARGS:-}
 echo session done
