@@ -125,7 +125,7 @@ static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budge
 #define POM_ENC_SAME 0                          // conflicts that keep the path resolved in place (A/B r05a: 3.8% slower on C3)
 #endif
 #ifndef POM_ENC_DPF
-#define POM_ENC_DPF 1                           // prefetch the next window's dictionary lines into L2
+#define POM_ENC_DPF 0                           // prefetch the next window's dictionary lines into L2 (A/B r05b: 10% slower)
 #endif
 #ifndef POM_ENC_PRIO_STEP
 #define POM_ENC_PRIO_STEP 8192
