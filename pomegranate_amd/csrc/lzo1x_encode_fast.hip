@@ -115,18 +115,6 @@ static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT <= 160 * 1024, "LDS budge
 #ifndef POM_ENC_PRIO
 #define POM_ENC_PRIO 1                          // one-wave kernel: wave priority by input bytes left
 #endif
-#ifndef POM_ENC_LAZYPRIO
-#define POM_ENC_LAZYPRIO 1                      // set the priority only when it steps down
-#endif
-#ifndef POM_ENC_WALK2
-#define POM_ENC_WALK2 1                         // path walk: unrolled, literal ranges by s_bfm_b64
-#endif
-#ifndef POM_ENC_SAME
-#define POM_ENC_SAME 0                          // conflicts that keep the path resolved in place (A/B r05a: 3.8% slower on C3)
-#endif
-#ifndef POM_ENC_DPF
-#define POM_ENC_DPF 0                           // prefetch the next window's dictionary lines into L2 (A/B r05b: 10% slower)
-#endif
 #ifndef POM_ENC_PRIO_STEP
 #define POM_ENC_PRIO_STEP 8192
 #endif
@@ -254,9 +242,6 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 #ifndef POM_ENC_BATCH
 #define POM_ENC_BATCH 1                          // the emit wave writes up to 64 tokens per pass
 #endif
-#ifndef POM_ENC_FARINV
-#define POM_ENC_FARINV 1
-#endif
 #ifndef POM_ENC_FWD
 #define POM_ENC_FWD 8                            // claim conflicts resolved in place per window
 #endif
@@ -276,13 +261,9 @@ __device__ __forceinline__ uint64_t bit_range(uint32_t off, uint32_t width)
 // v_ffbl_b32 of 0 is 0xFFFFFFFF, which a saturating add of 32i keeps, so the
 // minimum over the dwords of ffbl + 32i is the first differing bit: xor,
 // ffbl, add and a min3 half of the time per dword, no compare or select.
-#ifndef POM_ENC_FD
-#define POM_ENC_FD 1
-#endif
 template <int NW>
 __device__ __forceinline__ uint32_t first_diff(const uint32_t (&a)[NW], const uint32_t (&b)[NW])
 {
-#if POM_ENC_FD
     uint32_t m = 32 * NW;                           // (bit index of the first difference)
 #pragma unroll
     for (int i = 0; i < NW; i++) {
@@ -291,15 +272,6 @@ __device__ __forceinline__ uint32_t first_diff(const uint32_t (&a)[NW], const ui
         m = min(m, __builtin_elementwise_add_sat(f, 32u * i));          // (saturates: equal stays max)
     }
     return m >> 3;
-#else
-    uint32_t m = 4 * NW;
-#pragma unroll
-    for (int i = NW - 1; i >= 0; i--) {
-        const uint32_t x = a[i] ^ b[i];
-        m = x ? 4u * i + ((uint32_t)__builtin_ctz(x) >> 3) : m;
-    }
-    return m;
-#endif
 }
 
 // Match length from index k0 on (the first k0 bytes match), wave-parallel,
@@ -550,7 +522,6 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
     const uintptr_t pf_lines = (uintptr_t)in & ~(uintptr_t)127;
     const uintptr_t pf_last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
     uint32_t pf = 0, pf_acc = 0, pf_new = 0;
-    uint32_t dpf1 = 0, dpf2 = 0;                    // (POM_ENC_DPF) the next window's dictionary lines
     auto prefetch = [&](uint32_t at) {
         pf_acc ^= pf_new;
         pf_new = 0;
@@ -611,7 +582,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // (more input left) get the issue slots first, so the workgroups of
             // a CU finish together.  The priority steps down at most three
             // times a block: it is set again only once ip passes prio_ip.
-            if (FUSED && E->prio && (!POM_ENC_LAZYPRIO || ip >= prio_ip)) {
+            if (FUSED && E->prio && ip >= prio_ip) {
                 const uint32_t left = n - ip, st = POM_ENC_PRIO_STEP;
                 const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
                                                                   : left >= st ? 1u : 0u);
@@ -652,8 +623,6 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                                                    (pw[0] >> 16) & 0xFF, pw[0] >> 24);
             const uint32_t h2 = emit::slot_secondary(h1);
             const uint32_t e1 = D.get(h1), e2 = D.get(h2);
-            if (POM_ENC_DPF && GD && FUSED)
-                pf_new ^= dpf1 ^ dpf2;               // (their wait merges with the probes')
             const uint32_t w1 = active && e1 ? base + e1 - 1 : 0u;   // (positions >= 4: 0 stays "empty")
             const uint32_t w2 = active && e2 ? base + e2 - 1 : 0u;
             const uint64_t am = mask_lt(p, ip_end) | 1ull;      // (active)
@@ -667,17 +636,12 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             const bool v1 = active && w1 != 0 && p - w1 <= kM4MaxOffset;
             const bool v2 = v1 && w2 != 0 && p - w2 <= kM4MaxOffset;
             uint32_t c1w[kCmpW], c2w[kCmpW];        // (read unconditionally; used only if valid)
-#if POM_ENC_FARINV
             // (lanes without a valid candidate read past the block: range
             // checked, no memory request; the secondary candidate is only
             // ever compared when the primary one is more than M2_MAX_OFFSET
             // back, lib/minilzo.c:2946-2949)
             load_at<kCmpW, POM_CAND_AUX>(B, v1 ? w1 : kFarPos, c1w);
             load_at<kCmpW, POM_CAND_AUX>(B, v2 && p - w1 > kM2MaxOffset ? w2 : kFarPos, c2w);
-#else
-            load_at<kCmpW>(B, w1, c1w);
-            load_at<kCmpW>(B, w2, c2w);
-#endif
             const uint32_t b3 = pw[0] >> 24;
             // (selects, no branches)
             const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
@@ -711,38 +675,6 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // The path from lane `from` on (lanes below it stay as they are):
             // from `end`, the next match lane q -- the literal lanes end .. q-1
             // before it -- then on from q + its length.
-#if !POM_ENC_WALK2
-            auto walk = [&](uint32_t from) {
-                end = from;
-                while (end < nact) {
-                    if (STAMPS)
-                        acc[EC_PATHIT] += 1;
-                    const uint64_t rest = okm & (~0ull << end);
-                    const uint32_t q = rest ? (uint32_t)__builtin_ctzll(rest) : nact;
-                    const uint32_t lit_end = q < nact ? q : nact;
-                    if (lit_end > end)               // literal lanes end .. lit_end-1
-                        path |= (lit_end >= 64 ? ~0ull : ((1ull << lit_end) - 1)) & (~0ull << end);
-                    if (q >= nact) {
-                        end = nact;
-                        break;
-                    }
-                    path |= 1ull << q;
-                    mstart |= 1ull << q;
-                    uint32_t len = lane_read(mlen, q);
-                    if (len == kCmpB && n - (ip + q) > kCmpB) {
-                        if (STAMPS)
-                            acc[EC_EXTEND] += 1;
-                        len = extend_match(B, n, lane_read(cand, q), ip + q, kCmpB, l);
-                        if (STAMPS)
-                            acc[EC_EXTIT] += (len - kCmpB) / (4 * kWave) + 1;
-                        mlen = l == q ? len : mlen;
-                    }
-                    end = q + len;
-                    if (++nmatch >= POM_ENC_PATHMAX) // the window ends after this match
-                        break;
-                }
-            };
-#else
             auto walk = [&](uint32_t from) {
                 end = from;
 #pragma unroll
@@ -773,16 +705,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                     nmatch++;                        // (the window ends after the last one)
                 }
             };
-#endif
             walk(0);
-            // The next window's probe words, issued now (read again below when
-            // forwarding moves the window's end): after the claims, their
-            // hashes pull the next window's dictionary lines into L2.
-            uint32_t npw[kCmpW];
-            uint32_t npw_end = end;
-            if (POM_ENC_DPF && GD && FUSED)
-                load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
-
             ESTAMP(EP_PATH);
             // ---- exactness: claims among the path lanes, and forwarding ------
             // Path lane l read h1 (and h2 when use2) and writes slot.  The
@@ -793,12 +716,9 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // lane c, lowest first, is decided again: its entry is the position
             // of the last lower path lane j writing that slot -- less than 64
             // back, so the candidate passes the M2_MAX_OFFSET test -- and j's
-            // probe words are the candidate's bytes.  When the new decision
-            // leaves c's kind, length and written slot as they were (the path
-            // and the claims stand), the round goes on to the next conflicting
-            // lane; otherwise the path is walked again from c and the claims
-            // re-posted under a new tag.  After POM_ENC_FWD rounds the window
-            // ends at the next conflicting lane.
+            // probe words are the candidate's bytes.  The path is walked again
+            // from c and the claims re-posted under a new tag.  After
+            // POM_ENC_FWD rounds the window ends at the next conflicting lane.
             uint64_t resolved = 0, superseded = 0;   // (superseded: a later lane writes its slot)
             uint64_t um2 = wave_ballot(use2);        // lanes that read the secondary slot
             for (uint32_t round = 0;; round++) {
@@ -820,76 +740,50 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                     end = (uint32_t)__builtin_ctzll(cm);   // the window ends at a path lane
                     break;
                 }
-                bool moved = false;                  // the path changed: claims again
-                while (cm) {
-                    const uint32_t c = (uint32_t)__builtin_ctzll(cm);   // never lane 0
-                    cm &= cm - 1;
-                    if (STAMPS)
-                        acc[EC_FWD] += 1;
-                    resolved |= 1ull << c;
-                    const uint64_t below_c = (1ull << c) - 1;
-                    const uint64_t pm = path & below_c;  // exact path lanes below c
-                    const uint32_t h1c = lane_read(h1, c), h2c = lane_read(h2, c);
-                    const bool u2c = ((um2 >> c) & 1ull) != 0;
-                    const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
-                    const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (u2c ? ~0ull : 0ull);
-                    if (!wm1 && !wm2) {              // a claim-table alias: c was exact
-                        if (POM_ENC_SAME)
-                            continue;
-                        moved = true;                // (the old protocol: claims again)
-                        break;
-                    }
-                    const bool via2 = wm1 == 0;      // h1 unchanged, its test failed again: h2
-                    const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
-                    superseded |= 1ull << j;         // c writes j's slot after j
-                    uint32_t pj[kCmpW];
+                const uint32_t c = (uint32_t)__builtin_ctzll(cm);   // never lane 0
+                if (STAMPS)
+                    acc[EC_FWD] += 1;
+                resolved |= 1ull << c;
+                const uint64_t below_c = (1ull << c) - 1;
+                const uint64_t pm = path & below_c;      // exact path lanes below c
+                const uint32_t h1c = lane_read(h1, c), h2c = lane_read(h2, c);
+                const bool u2c = ((um2 >> c) & 1ull) != 0;
+                const uint64_t wm1 = wave_ballot(slot == h1c) & pm;
+                const uint64_t wm2 = wave_ballot(slot == h2c) & pm & (u2c ? ~0ull : 0ull);
+                if (!wm1 && !wm2)                        // a claim-table alias: c was exact
+                    continue;                            // (claims again)
+                const bool via2 = wm1 == 0;              // h1 unchanged, its test failed again: h2
+                const uint32_t j = 63u - (uint32_t)__builtin_clzll(via2 ? wm2 : wm1);
+                superseded |= 1ull << j;                 // c writes j's slot after j
+                uint32_t pj[kCmpW];
 #pragma unroll
-                    for (int i = 0; i < kCmpW; i++)
-                        pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)pw[i]);
-                    uint32_t mc = first_diff<kCmpW>(pj, pw);
-                    mc = mc < n - p ? mc : n - p;
-                    const bool isc = l == c;
-                    const bool nok = ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0;
-                    const bool ook = ((okm >> c) & 1ull) != 0;
-                    const uint64_t nokm = wave_ballot(isc ? nok : ok);
-                    const uint32_t omc = lane_read(mlen, c), nmc = lane_read(mc, c);
-                    // the same kind, length (not one an extension decides) and slot
-                    const bool same = ((nokm >> c) & 1ull) == ook && via2 == u2c &&
-                                      (!ook || (nmc == omc && omc < kCmpB));
-                    ok = isc ? nok : ok;
-                    mlen = isc ? mc : mlen;
-                    cand = isc ? ip + j : cand;
-                    slot = isc ? (via2 ? h2 : h1) : slot;
-                    use2 = isc ? via2 : use2;
-                    um2 = via2 ? um2 | (1ull << c) : um2 & ~(1ull << c);
-                    okm = nokm;
-                    if (POM_ENC_SAME && same)
-                        continue;                    // path and claims stand: the next conflict
-                    path &= below_c;
-                    mstart &= below_c;
-                    nmatch = (uint32_t)__builtin_popcountll(mstart);
-                    walk(c);
-                    moved = true;
-                    break;
-                }
-                if (!moved)
-                    break;                           // every conflict resolved in place: exact
+                for (int i = 0; i < kCmpW; i++)
+                    pj[i] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)pw[i]);
+                uint32_t mc = first_diff<kCmpW>(pj, pw);
+                mc = mc < n - p ? mc : n - p;
+                const bool isc = l == c;
+                const bool nok = ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0;
+                ok = isc ? nok : ok;
+                mlen = isc ? mc : mlen;
+                cand = isc ? ip + j : cand;
+                slot = isc ? (via2 ? h2 : h1) : slot;
+                use2 = isc ? via2 : use2;
+                um2 = via2 ? um2 | (1ull << c) : um2 & ~(1ull << c);
+                okm = wave_ballot(ok);
+                path &= below_c;
+                mstart &= below_c;
+                nmatch = (uint32_t)__builtin_popcountll(mstart);
+                walk(c);
             }
             if (STAMPS) {                            // (why the window ended)
                 acc[EC_C2NEED] += end > 64 ? 1 : 0;  // a match crossing its last lane
                 acc[EC_C2MATCH] += nmatch >= POM_ENC_PATHMAX ? 1 : 0;   // the path cap
             }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
-
-            if (!(POM_ENC_DPF && GD && FUSED) || end != npw_end)
-                load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
-            npw_end = end;
-            if (POM_ENC_DPF && GD && FUSED) {
-                const uint32_t nh1 = emit::slot_primary(npw[0] & 0xFF, (npw[0] >> 8) & 0xFF,
-                                                        (npw[0] >> 16) & 0xFF, npw[0] >> 24);
-                dpf1 = D.get(nh1);                   // (line prefetch: the values are not used)
-                dpf2 = D.get(emit::slot_secondary(nh1));
-            }
+            // The next window's probe words, issued now: ahead of the token
+            // and dictionary writes.
+            uint32_t npw[kCmpW];
+            load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
 
             ESTAMP(EP_CLAIM);
             // ---- tokens for the matches before the cut ------------------------
