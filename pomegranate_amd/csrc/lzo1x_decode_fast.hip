@@ -146,7 +146,8 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t src[kSrcDw];     // this window's literal spans and far match sources
     uint4 wop[kWave];         // window op: {o, source base (| kLitFlag: linear), first 16-B chunk, L}
     uint2 wper[kWave];        // window op: {period, floor((2^32-1)/period)}
-    uint32_t flags[kWave + 4];  // per-step chunk tags (src_issue: per-dword byte flags); [kWave]: trash
+    uint32_t flags[kWave + 4];  // per-step chunk tags (src_issue: per-dword byte flags); [kWave]: spare
+                              // (+4: the fields after it stay 16-byte aligned)
     // v_perm selectors of the period-p pattern expansion (p < 16): byte i of
     // psel[0][p] selects pattern byte i mod p from dwords 1:0 (12 = zero when
     // it lies in 2:3), psel[1][p] the same from dwords 3:2.  A chunk of phase
@@ -167,7 +168,6 @@ struct __attribute__((aligned(16))) FastLds {
     uint32_t opset;           // this workgroup's op-slot set (from the pool)
     uint32_t done;            // waves done with the block (the second one closes it)
     uint32_t why;             // executor's refusal reason
-    uint32_t trash[4];        // target of the partial-chunk writes a lane does not make
 };
 
 constexpr uint32_t kRingOff = 0;                                  // offsetof(FastLds, ring)
@@ -177,6 +177,8 @@ static_assert(offsetof(FastLds, src) == kSrcOff, "layout");
 constexpr uint32_t kLdsMask = 0x3FFF;                              // LDS-linear address space
 static_assert(sizeof(FastLds) <= kLdsMask + 1 && kLdsMask + 1 == kLinHbm,
               "linear LDS addresses are masked to 16 KiB");
+static_assert(offsetof(FastLds, psel) % 16 == 0 && offsetof(FastLds, stage) % 16 == 0,
+              "16-byte LDS reads of the selectors and the staging stay aligned");
 // 16 blocks per CU share its 160 KiB of LDS
 static_assert(sizeof(FastLds) * 2 * POM_WAVES_PER_EU <= 160 * 1024, "LDS budget");
 
@@ -550,48 +552,6 @@ __device__ __forceinline__ void lds_write1(uint32_t a, uint32_t v)
     asm volatile("ds_write_b8 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
-#ifndef POM_DEC_R5
-#define POM_DEC_R5 1                             // round-5 step: no exec-masked branches in the byte moving
-#endif
-#ifndef POM_DEC_R5_BASE
-#define POM_DEC_R5_BASE POM_DEC_R5               // LDS bases from one readfirstlane
-#endif
-#ifndef POM_DEC_R5_TAG
-#define POM_DEC_R5_TAG POM_DEC_R5                // chunk tags written without a branch
-#endif
-#ifndef POM_DEC_R5_MOD
-#define POM_DEC_R5_MOD POM_DEC_R5                // period reduction without a branch
-#endif
-#ifndef POM_DEC_R5_MERGE
-#define POM_DEC_R5_MERGE POM_DEC_R5              // two-read merge masks without branches
-#endif
-#ifndef POM_DEC_R5_WRITE
-#define POM_DEC_R5_WRITE 0                       // partial-chunk writes to a trash slot (A/B r05a: 4% slower)
-#endif
-// The first len (<= 16) bytes of v at LDS address a, without exec branches:
-// every piece (b128 for a whole chunk, else b64/b32/b16/b8) is written by
-// every lane, at a, or at the trash slot t when the lane's chunk does not
-// take it; a piece no lane takes is skipped by a uniform branch.
-__device__ __forceinline__ __attribute__((unused)) void lds_write_part_bf(uint32_t a, uint4 v, uint32_t len, uint32_t t)
-{
-    const bool f16 = len == 16u, f8 = (len & 8u) != 0, f4 = (len & 4u) != 0, f2 = (len & 2u) != 0,
-               f1 = (len & 1u) != 0;
-    if (__builtin_amdgcn_uicmp(len, 16u, 32))         // (ballot of len == 16)
-        lds_write16(f16 ? a : t, v);
-    const uint32_t w0 = f8 ? v.z : v.x, w1 = f8 ? v.w : v.y;
-    const uint32_t a8 = a + (len & 8u);
-    if (__builtin_amdgcn_uicmp(len & 8u, 0u, 33) & __builtin_amdgcn_uicmp(len, 16u, 33))
-        lds_write8(f8 && !f16 ? a : t, v.x, v.y);
-    const uint32_t x4 = f4 ? w1 : w0;
-    const uint32_t a4 = a8 + (len & 4u);
-    if (__builtin_amdgcn_uicmp(len & 4u, 0u, 33))
-        lds_write4(f4 ? a8 : t, w0);
-    const uint32_t a2 = a4 + (len & 2u);
-    if (__builtin_amdgcn_uicmp(len & 2u, 0u, 33))
-        lds_write2(f2 ? a4 : t, x4);
-    if (__builtin_amdgcn_uicmp(len & 1u, 0u, 33))
-        lds_write1(f1 ? a2 : t, f2 ? x4 >> 16 : x4);
-}
 
 // The first len (<= 16) bytes of v at LDS address a: one b128 for a whole
 // chunk, else b64/b32/b16/b8 pieces.
@@ -1467,19 +1427,12 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     }
 
     uint64_t tmark = STAMPS ? __builtin_amdgcn_s_memtime() : 0;
-#if POM_DEC_R5_BASE
     // (LDS addresses as offsets from one readfirstlane'd base: the compiler
     // otherwise re-derives each generic-to-LDS cast, with its null check, in
     // every step)
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_off(&S));
     const uint32_t psel0 = base + (uint32_t)offsetof(FastLds, psel);
     const uint32_t psel1 = psel0 + (uint32_t)sizeof(S.psel[0]);
-    [[maybe_unused]] const uint32_t trash = base + (uint32_t)offsetof(FastLds, trash);
-#else
-    const uint32_t base = lds_off(&S);
-    const uint32_t psel0 = lds_off(&S.psel[0][0][0]), psel1 = lds_off(&S.psel[1][0][0]);
-    [[maybe_unused]] const uint32_t trash = lds_off(&S.trash[0]);
-#endif
     uint32_t carry = 0;                        // output produced so far
     uint32_t issued_seen = 0, landed_seen = 0; // last `issued` / `landed` read
     uint32_t tag = 0;                          // step counter for the chunk tags
@@ -1661,12 +1614,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     // before chunk C + l (a ballot and mbcnt, no scan).
                     tag++;
                     const uint32_t tagv = tag | 0x80000000u;   // src_issue's byte flags never set bit 31
-#if POM_DEC_R5_TAG
                     S.flags[starter && cs >= C && cs < C + kWave ? cs - C : (uint32_t)kWave] = tagv;
-#else
-                    if (starter && cs >= C && cs < C + kWave)
-                        S.flags[cs - C] = tagv;
-#endif
                     wave_order();
                     const bool st0 = S.flags[l] == tagv;
                     const uint64_t Mb = wave_ballot(st0);
@@ -1713,17 +1661,9 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     const uint32_t p = pr.x;
                     const bool lin = (op.y & kLitFlag) != 0;
                     const uint32_t bb = op.y & ~kLitFlag;
-                    uint32_t r0 = k16;
-#if POM_DEC_R5_MOD
                     // (p == 0: the inverse is 0, so r0 stays k16 without a branch)
-                    r0 = k16 - p * (uint32_t)__umulhi(k16, pr.y);
+                    uint32_t r0 = k16 - p * (uint32_t)__umulhi(k16, pr.y);
                     r0 = min(r0, r0 - p);
-#else
-                    if (p) {
-                        r0 = k16 - p * (uint32_t)__umulhi(k16, pr.y);
-                        r0 = min(r0, r0 - p);
-                    }
-#endif
                     const bool small = p != 0 && p < 16u;       // pattern expansion
                     const uint32_t n1 = p - r0;                 // (p >= 16) bytes before the wrap
                     const bool two = p >= 16u && n1 < len;      // the chunk wraps the period
@@ -1776,7 +1716,6 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     if (any_two) {
                         // bytes i < n1 from vA, the rest from vB
                         const uint32_t n = two ? n1 : 16u;
-#if POM_DEC_R5_MERGE
                         // bytes below n (1 <= n <= 16) as two 64-bit masks, no
                         // branches: (2 << (8k - 1)) - 1 is k bytes for k = 1..8
                         const uint32_t nl = n < 8u ? n : 8u, nh = n > 8u ? n - 8u : 1u;
@@ -1784,12 +1723,6 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                         const uint64_t mhi = n > 8u ? (2ull << (8u * nh - 1u)) - 1ull : 0ull;
                         const uint32_t m0 = (uint32_t)mlo, m1 = (uint32_t)(mlo >> 32);
                         const uint32_t m2 = (uint32_t)mhi, m3 = (uint32_t)(mhi >> 32);
-#else
-                        const uint32_t m0 = n >= 4 ? ~0u : (1u << (8 * n)) - 1u;
-                        const uint32_t m1 = n >= 8 ? ~0u : n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1u;
-                        const uint32_t m2 = n >= 12 ? ~0u : n <= 8 ? 0u : (1u << (8 * (n - 8))) - 1u;
-                        const uint32_t m3 = n >= 16 ? ~0u : n <= 12 ? 0u : (1u << (8 * (n - 12))) - 1u;
-#endif
                         v.x = (vA.x & m0) | (vB.x & ~m0);
                         v.y = (vA.y & m1) | (vB.y & ~m1);
                         v.z = (vA.z & m2) | (vB.z & ~m2);
@@ -1806,18 +1739,11 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     // ---- destination: the ring at x -----------------------------
                     const uint32_t xd = x & kRingMask;
                     const bool wcross = live && xd + len > kRing;
-#if POM_DEC_R5_WRITE
-                    const uint32_t wlen = live && !wcross ? len : 0u;
-                    lds_write_part_bf(base + xd, v, wlen, trash);
-                    if (mask_lt(xd, 16u) & mask_lt(0u, wlen))   // keep the mirror of ring[0, 16)
-                        lds_write_part_bf(base + kRing + xd, v, xd < 16u ? wlen : 0u, trash);
-#else
                     if (live && !wcross) {
                         lds_write_part(base + xd, v, len);
                         if (xd < 16u)                  // keep the mirror of ring[0, 16)
                             lds_write_part(base + kRing + xd, v, len);
                     }
-#endif
                     if (mask_lt(kRing, xd + len)) {     // (wcross; len is 0 off the step)
                         if (wcross) {                  // destination wraps the ring end
                             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};

@@ -567,7 +567,8 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
         uint32_t ip = 4;
         uint32_t base = 0;                          // dictionary position base
         uint32_t wtag = 0xFFFFFEu;                  // claim tag of the window (one per window, > 0)
-        uint32_t prio_ip = 0;                       // (FUSED priority) next ip at which it steps down
+        // (FUSED priority) next ip at which it steps down; never without priority
+        uint32_t prio_ip = FUSED && E->prio ? 0u : 0xFFFFFFFFu;
         // Probe words of the window (position ip + l): the next window's are
         // read as soon as its start is known, ahead of the token and
         // dictionary writes.
@@ -582,7 +583,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             // (more input left) get the issue slots first, so the workgroups of
             // a CU finish together.  The priority steps down at most three
             // times a block: it is set again only once ip passes prio_ip.
-            if (FUSED && E->prio && ip >= prio_ip) {
+            if (FUSED && ip >= prio_ip) {
                 const uint32_t left = n - ip, st = POM_ENC_PRIO_STEP;
                 const uint32_t q = __builtin_amdgcn_readfirstlane(left >= 3u * st ? 3u : left >= 2u * st ? 2u
                                                                   : left >= st ? 1u : 0u);

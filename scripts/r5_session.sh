@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-5 GPU session: build, parity tests, A/B of the C3 kernels against the
-# round-4 sources (scripts/ab/*_base.hip), smoke, bench.  Each GPU step has its
-# own time limit; a crash or timeout ends the session.
+# Round-5 GPU session: build, parity tests, A/B of the C3 kernels against
+# variant libraries (scripts/ab/lib_NAME.so from scripts/ab_build.sh, listed in
+# AB), smoke, bench.  Each GPU step has its own time limit; a crash or timeout
+# ends the session.
 set -u
 OUT=${OUT:-gpurun_out/r5}
 mkdir -p "$OUT"
