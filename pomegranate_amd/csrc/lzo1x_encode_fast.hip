@@ -673,24 +673,29 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             uint64_t path = 0, mstart = 0;
             uint32_t end = 0;                        // lane where the path leaves the window
             uint32_t nmatch = 0;
-            // The path from lane `from` on (lanes below it stay as they are):
-            // from `end`, the next match lane q -- the literal lanes end .. q-1
-            // before it -- then on from q + its length.
+            // The path through the window from lane `from` on (lanes below it
+            // stay as they are): from `end`, the next match lane q -- the
+            // literal lanes end .. q-1 before it -- then on from q + its
+            // length.  rem: the ok lanes at or after `end` (empty once the path
+            // leaves the window: ok lanes are active ones).
             auto walk = [&](uint32_t from) {
                 end = from;
+                uint64_t rem = okm & (~0ull << from);            // (from < 64)
+                uint32_t nm = nmatch;
 #pragma unroll
                 for (int it = 0; it < POM_ENC_PATHMAX; it++) {
-                    if (end >= nact || nmatch >= POM_ENC_PATHMAX)
+                    if (nm >= POM_ENC_PATHMAX)
                         break;
-                    if (STAMPS)
-                        acc[EC_PATHIT] += 1;
-                    const uint64_t rest = okm & (~0ull << end);     // (end < 64 here)
-                    if (!rest) {                     // literal lanes to the last active one
-                        path |= nact - end >= 64 ? ~0ull : bit_range(end, nact - end);
-                        end = nact;
+                    if (!rem) {
+                        if (end < nact) {            // literal lanes to the last active one
+                            path |= nact - end >= 64 ? ~0ull : bit_range(end, nact - end);
+                            end = nact;
+                        }
                         break;
                     }
-                    const uint32_t q = (uint32_t)__builtin_ctzll(rest);   // (< nact: ok lanes are active)
+                    if (STAMPS)
+                        acc[EC_PATHIT] += 1;
+                    const uint32_t q = (uint32_t)__builtin_ctzll(rem);
                     path |= bit_range(end, q - end) | (1ull << q);        // (q - end < 64)
                     mstart |= 1ull << q;
                     uint32_t len = lane_read(mlen, q);
@@ -703,8 +708,11 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                         mlen = l == q ? len : mlen;
                     }
                     end = q + len;
-                    nmatch++;                        // (the window ends after the last one)
+                    nm++;                            // (the window ends after the last one)
+                    const uint32_t e = end < 64u ? end : 64u;   // (past the window: a width-0 mask)
+                    rem &= bit_range(e, 64u - e);
                 }
+                nmatch = nm;
             };
             walk(0);
             ESTAMP(EP_PATH);
