@@ -1546,6 +1546,11 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             // sequential fixed point on ITB streams (600 -> 205 batches per
             // 64 KiB block).
             const uint32_t o_first = lane_read(o, 0);
+            // periods' inverses for the mod by mulhi (forwarding moves sources,
+            // never periods: the steps use them too)
+            uint32_t inv = 0;
+            if (wave_ballot(dp != 0))
+                inv = dp ? 0xFFFFFFFFu / dp : 0u;
             for (int round = 0; round < POM_FWD_ROUNDS; round++) {
                 const uint32_t span = dp ? dp : L;
                 const bool need = l < nwin && !(db & kLitFlag) && db + span > o_first;
@@ -1565,12 +1570,11 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                 const uint32_t kL = (uint32_t)__shfl((int)L, (int)k2, kWave);
                 const uint32_t kb = (uint32_t)__shfl((int)db, (int)k2, kWave);
                 const uint32_t kp = (uint32_t)__shfl((int)dp, (int)k2, kWave);
-                bool ok = need && k2 < l && ko <= db && db + span <= ko + kL;
+                const uint32_t kinv = (uint32_t)__shfl((int)inv, (int)k2, kWave);
                 uint32_t r = db - ko;
-                if (ok && kp) {
-                    r %= kp;
-                    ok = r + span <= kp;
-                }
+                const uint32_t rr = r - kp * (uint32_t)__umulhi(r, kinv);   // (kp == 0: kinv == 0, rr == r)
+                r = min(rr, rr - kp);                  // r mod kp
+                const bool ok = need && k2 < l && ko <= db && db + span <= ko + kL && (!kp || r + span <= kp);
                 if (ok)
                     db = kb + r;                       // (kb carries k's linear flag)
             }
@@ -1581,9 +1585,6 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             const bool outsrc = l < nwin && !(db & kLitFlag);
             const uint32_t span = dp ? dp : L;
             const uint32_t send = outsrc ? db + span : 0u;
-            uint32_t inv = 0;                          // mod by mulhi; only overlapping matches
-            if (wave_ballot(dp != 0))
-                inv = dp ? 0xFFFFFFFFu / dp : 0u;
             // Chunks: op j covers the window's 16-byte chunks cs .. cs +
             // ceil(L/16) - 1, each up to 16 bytes of that op alone.
             const uint32_t nch = l < nwin ? (L + 15u) >> 4 : 0u;

@@ -646,7 +646,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             const uint32_t b3 = pw[0] >> 24;
             // (selects, no branches)
             const bool c1pass = v1 && (p - w1 <= kM2MaxOffset || (c1w[0] >> 24) == b3);
-            bool use2 = v1 && !c1pass;               // the secondary slot is read and written
+            const bool use2 = v1 && !c1pass;         // the secondary slot is read and written
             const bool c2pass = use2 && v2 && (p - w2 <= kM2MaxOffset || (c2w[0] >> 24) == b3);
             const bool tm = c1pass || c2pass;
             uint32_t slot = use2 ? h2 : h1, cand = c2pass ? w2 : w1;
@@ -655,7 +655,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             for (int i = 0; i < kCmpW; i++)
                 cw[i] = c2pass ? c2w[i] : c1w[i];
             // try_match (:2962-2971), then the match length as far as kCmpB bytes
-            bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
+            const bool ok = tm && ((cw[0] ^ pw[0]) & 0xFFFFFFu) == 0;
             uint32_t mlen = first_diff<kCmpW>(cw, pw);
             mlen = mlen < n - p ? mlen : n - p;
 
@@ -771,14 +771,15 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 uint32_t mc = first_diff<kCmpW>(pj, pw);
                 mc = mc < n - p ? mc : n - p;
                 const bool isc = l == c;
-                const bool nok = ((pj[0] ^ pw[0]) & 0xFFFFFFu) == 0;
-                ok = isc ? nok : ok;
+                const uint64_t bitc = 1ull << c;
+                // (lane c's new decision goes into the lane masks; ok and use2
+                // themselves are not read again)
+                const uint64_t nokm = __builtin_amdgcn_uicmp((pj[0] ^ pw[0]) & 0xFFFFFFu, 0u, 32);
+                okm = (okm & ~bitc) | (nokm & bitc);
+                um2 = via2 ? um2 | bitc : um2 & ~bitc;
                 mlen = isc ? mc : mlen;
                 cand = isc ? ip + j : cand;
                 slot = isc ? (via2 ? h2 : h1) : slot;
-                use2 = isc ? via2 : use2;
-                um2 = via2 ? um2 | (1ull << c) : um2 & ~(1ull << c);
-                okm = wave_ballot(ok);
                 path &= below_c;
                 mstart &= below_c;
                 nmatch = (uint32_t)__builtin_popcountll(mstart);
