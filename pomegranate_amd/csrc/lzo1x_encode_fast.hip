@@ -165,15 +165,19 @@ struct Dict {
 __device__ __forceinline__ uint32_t lane_id() { return emit::lane(); }
 __device__ __forceinline__ uint32_t claim_index(uint32_t slot) { return (slot ^ (slot >> 9)) & (kClaim - 1); }
 
-// Inclusive prefix sum over the wave.
+// Inclusive prefix sum over the wave: DPP row shifts inside each 16-lane row,
+// then the row totals via readlane (no LDS round trip; lzo1x_decode_fast.hip
+// scans the same way).
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v)
 {
-    const uint32_t l = lane_id();
-#pragma unroll
-    for (uint32_t d = 1; d < (uint32_t)kWave; d <<= 1) {
-        const uint32_t u = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((l - d) << 2), (int)v);
-        v += l >= d ? u : 0u;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31),
+                   r2 = __builtin_amdgcn_readlane(v, 47);
+    const uint32_t row = lane_id() >> 4;
+    v += (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
     return v;
 }
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
@@ -356,10 +360,11 @@ struct Emitter {
         const uint32_t iadv = wave_incl_sum(adv);
         const uint32_t isz = wave_incl_sum(sz);
         const uint32_t pk = pos + iadv - adv;              // input position of token k
-        const uint32_t budget = e.smask + 1 - (e.op - e.flushed) - 4;
-        const bool fits = k < avail && L != 0 && r <= kLitMax && (shortlen || L - lim <= 255) &&
-                          t.x == pk && r <= n - pk && L <= n - pk - r && d != 0 && d <= pk + r &&
-                          d <= kM4MaxOffset && isz <= budget;
+        const uint32_t budget = e.smask + 1 - (e.op - e.flushed) - 4 - kLitMax;   // (- kLitMax: see the literals)
+        // (every test evaluated: no short-circuit exec-mask cascade)
+        const bool fits = (k < avail) & (L != 0) & (r <= kLitMax) & (shortlen | (L - lim <= 255)) &
+                          (t.x == pk) & (r <= n - pk) & (L <= n - pk - r) & (d != 0) & (d <= pk + r) &
+                          (d <= kM4MaxOffset) & (isz <= budget);
         const uint64_t bad = wave_ballot(!fits);
         const uint32_t nb = bad ? (uint32_t)__builtin_ctzll(bad) : (uint32_t)kWave;
         if (nb == 0)
@@ -373,8 +378,6 @@ struct Emitter {
         if (k == 0 && r >= 1 && r <= 3)
             st[(e.op - 2) & m] |= (uint8_t)r;
         wave_order();
-        if (act && hdr)
-            st[o & m] = (uint8_t)(r - 3);
         uint32_t lw[kLitMax / 4];
         {
             const uint32_t a = (act && r ? t.x : kFarPos) + B.sh0;
@@ -387,10 +390,20 @@ struct Emitter {
                 lw[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], a & 3u);
         }
         const uint32_t ol = o + hdr;
+        // Literals: kLitMax bytes per lane whatever the run's length, highest
+        // first, so no write is exec-masked per byte.  A byte past a lane's run
+        // belongs to a later token: its owner writes it later in this loop (a
+        // smaller index), or the headers and match bytes below do; the last
+        // lane's extra bytes land in the ring's free space (the budget keeps
+        // kLitMax spare).
+        if (act) {
 #pragma unroll
-        for (uint32_t i = 0; i < kLitMax; i++)
-            if (act && i < r)
+            for (int i = (int)kLitMax - 1; i >= 0; i--)
                 st[(ol + i) & m] = (uint8_t)(lw[i >> 2] >> (8 * (i & 3)));
+        }
+        wave_order();
+        if (act && hdr)
+            st[o & m] = (uint8_t)(r - 3);
         // the match (lib/minilzo.c:3064-3145), the next run's length ORed in
         const uint32_t oo = near ? d - 1 : d - 0x4000;
         const uint32_t dlo = (oo & 63) << 2, dhi = oo >> 6;
