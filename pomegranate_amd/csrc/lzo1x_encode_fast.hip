@@ -67,6 +67,9 @@ constexpr uint32_t kFarPos = 0xC0000000u;        // a read position past every b
 #ifndef POM_ENC_AHEAD
 #define POM_ENC_AHEAD 2048                      // bytes the emit wave pulls into L2 ahead of the parse
 #endif
+#ifndef POM_ENC_AHEAD1
+#define POM_ENC_AHEAD1 0                        // the one-wave kernel's own read-ahead (0: none)
+#endif
 
 // The dictionary lives in LDS (4 blocks per CU: it is 32 KiB) or, with
 // scratch from the caller, in global memory: 32 KiB per resident workgroup,
@@ -512,7 +515,7 @@ constexpr int kEncStampSlots = 16;
 // batches than an eager emit wave gets) or the queue has no room, and at the
 // end -- and pulls the lines ahead of the parse into L2 as the emit wave does.
 #ifndef POM_ENC_DRAIN
-#define POM_ENC_DRAIN 32
+#define POM_ENC_DRAIN 48
 #endif
 template <bool STAMPS, bool GD, bool FUSED = false>
 __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, uint32_t n, uint32_t l,
@@ -529,16 +532,17 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
     } while (0)
     uint32_t tp = 0;                                // tokens produced
     uint32_t cons_seen = 0;
-    // (FUSED) lines up to POM_ENC_AHEAD bytes past the window go to L2, one
-    // dword per 128-B line; the loaded words are folded in a window later, so
-    // the parse never waits on them.
+    // (FUSED, POM_ENC_AHEAD1) lines up to that many bytes past the window go
+    // to L2, one dword per 128-B line.  Off by default: a wave's loads retire
+    // in order, so the window after such a load waits for its miss, and the
+    // distance (0 / 2 / 4 KiB) moved C3 by under 1%.
     const uintptr_t pf_lines = (uintptr_t)in & ~(uintptr_t)127;
     const uintptr_t pf_last = ((uintptr_t)in + n - 1) & ~(uintptr_t)3;
     uint32_t pf = 0, pf_acc = 0, pf_new = 0;
     auto prefetch = [&](uint32_t at) {
         pf_acc ^= pf_new;
         pf_new = 0;
-        const uint32_t ahead = at + POM_ENC_AHEAD;
+        const uint32_t ahead = at + POM_ENC_AHEAD1;
         const uint32_t want = ahead < n + 127 ? ahead : n + 127;
         for (; pf < want; pf += 128 * kWave) {
             const uintptr_t a = pf_lines + pf + 128 * l;
@@ -624,12 +628,10 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 wave_order();
                 base = nb;
             }
-            if (POM_ENC_AHEAD) {
-                if (FUSED)
-                    prefetch(ip);
-                else
-                    S.ip = ip;
-            }
+            if (FUSED && POM_ENC_AHEAD1)
+                prefetch(ip);
+            else if (!FUSED && POM_ENC_AHEAD)
+                S.ip = ip;
             const uint32_t p = ip + l;
             const bool active = l == 0 || p < ip_end;   // the first probe always runs
             // (every lane probes; an inactive one ends with no candidate)
