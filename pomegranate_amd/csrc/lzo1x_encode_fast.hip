@@ -19,8 +19,8 @@
 //    the exact prefix the greedy parse proceeds as the reference does: the
 //    first matching lane emits a match, the lanes it covers are skipped (they
 //    neither probe nor update the dictionary), and the lane right after it
-//    continues -- several matches per window.  Candidate bytes and a 16-byte
-//    match compare come in one round trip per window; only matches of 16
+//    continues -- several matches per window.  Candidate bytes and a 28-byte
+//    match compare come in one round trip per window; only matches of 28
 //    bytes or more need a wave-parallel extension.  The parse wave only emits
 //    tokens (literal run, match) into an LDS queue.
 //
@@ -241,7 +241,7 @@ __device__ __forceinline__ void load_at(const BlockSrc& B, uint32_t pos, uint32_
 }
 
 #ifndef POM_ENC_CMP
-#define POM_ENC_CMP 8                            // dwords compared in the window round trip
+#define POM_ENC_CMP 7                            // dwords compared in the window round trip (A/B r05q: 6 / 7 / 8 / 10)
 #endif
 #ifndef POM_ENC_PATHMAX
 #define POM_ENC_PATHMAX 6                        // matches the path walk takes per window
@@ -513,7 +513,7 @@ constexpr int kEncStampSlots = 16;
 // FUSED (one-wave kernel): the parse wave runs the emitter E itself -- it
 // drains the token queue once POM_ENC_DRAIN tokens are pending (larger emit
 // batches than an eager emit wave gets) or the queue has no room, and at the
-// end -- and pulls the lines ahead of the parse into L2 as the emit wave does.
+// end.
 #ifndef POM_ENC_DRAIN
 #define POM_ENC_DRAIN 48
 #endif
