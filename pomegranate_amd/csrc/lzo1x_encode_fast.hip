@@ -730,6 +730,12 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 nmatch = nm;
             };
             walk(0);
+            // The next window's probe words, issued from this first walk's end
+            // (again below only if forwarding moves the end): ahead of the
+            // claims, the token and the dictionary writes.
+            uint32_t npw[kCmpW];
+            const uint32_t end0 = end;
+            load_at<kCmpW, POM_PW_AUX>(B, ip + end0 + l, npw);
             ESTAMP(EP_PATH);
             // ---- exactness: claims among the path lanes, and forwarding ------
             // Path lane l read h1 (and h2 when use2) and writes slot.  The
@@ -805,10 +811,8 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 acc[EC_C2MATCH] += nmatch >= POM_ENC_PATHMAX ? 1 : 0;   // the path cap
             }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
-            // The next window's probe words, issued now: ahead of the token
-            // and dictionary writes.
-            uint32_t npw[kCmpW];
-            load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
+            if (end != end0)
+                load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
 
             ESTAMP(EP_CLAIM);
             // ---- tokens for the matches before the cut ------------------------

@@ -3,19 +3,20 @@
 # library build (GPU box): scripts/sq_changes.sh TAG NAME...  with
 # scripts/ab/lib_NAME.so built beforehand (scripts/ab_build.sh).  Per block,
 # 4096 x 64 KiB ITB blocks; summary on stdout and in gpurun_out/sqchg_TAG/.
+# PMC="..." replaces the counter set (one pass; all its counters are listed).
 set -u
 TAG=${1:?tag}; shift
 OUT=gpurun_out/sqchg_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_INST_ANY"
+SQ=${PMC:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_INST_ANY"}
 for v in "$@"; do
   timeout -s KILL 120 rocprofv3 --pmc $SQ --kernel-include-regex 'encode_(fast|gdict)' -d $OUT/$v -o sq --output-format csv -- python3 scripts/run_decode.py --op encode --reps 5 --lib scripts/ab/lib_$v.so > $OUT/$v.log 2>&1 || { echo "$v failed"; tail -5 $OUT/$v.log; exit 1; }
 done
-python3 - "$OUT" "$@" <<'PY'
+python3 - "$OUT" "$@" <<PY
 import csv, collections, glob, sys
 out, names = sys.argv[1], sys.argv[2:]
-keys = ["SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_INSTS_BRANCH", "SQ_INSTS_LDS", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"]
+keys = "${PMC:-SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES}".split()
 print("| build | " + " | ".join(k[3:] for k in keys) + " |")
 print("|---" * (len(keys) + 1) + "|")
 for v in names:
