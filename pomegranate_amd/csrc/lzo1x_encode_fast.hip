@@ -730,12 +730,15 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 nmatch = nm;
             };
             walk(0);
-            // The next window's probe words, issued from this first walk's end
-            // (again below only if forwarding moves the end): ahead of the
-            // claims, the token and the dictionary writes.
+            // The next window's probe words.  One-wave kernel: issued from this
+            // first walk's end (again below only if forwarding moves the end),
+            // ahead of the claims (C3 compress -1%).  The lone-block kernels
+            // issue them after the claims: there an early load holds up the
+            // re-walks' extension loads behind it (lone 64 KiB 655 -> 675 us).
             uint32_t npw[kCmpW];
             const uint32_t end0 = end;
-            load_at<kCmpW, POM_PW_AUX>(B, ip + end0 + l, npw);
+            if (FUSED)
+                load_at<kCmpW, POM_PW_AUX>(B, ip + end0 + l, npw);
             ESTAMP(EP_PATH);
             // ---- exactness: claims among the path lanes, and forwarding ------
             // Path lane l read h1 (and h2 when use2) and writes slot.  The
@@ -811,7 +814,7 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 acc[EC_C2MATCH] += nmatch >= POM_ENC_PATHMAX ? 1 : 0;   // the path cap
             }
             const uint64_t keep = end >= 64 ? ~0ull : ((1ull << end) - 1);
-            if (end != end0)
+            if (!FUSED || end != end0)
                 load_at<kCmpW, POM_PW_AUX>(B, ip + end + l, npw);
 
             ESTAMP(EP_CLAIM);
