@@ -1363,13 +1363,14 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     uint32_t* __restrict__ fallback, uint32_t* __restrict__ fallback_ids,
     uint2* __restrict__ ops, uint32_t nblocks,
     uint32_t prio_from, uint64_t* __restrict__ stamps, uint32_t* __restrict__ pool,
-    unsigned long long* __restrict__ ring, uint32_t nsets)
+    unsigned long long* __restrict__ ring, uint32_t nsets, const uint32_t* __restrict__ order)
 {
     __shared__ FastLds S;
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks)
+    const uint32_t bi = blockIdx.x;                  // start order
+    if (bi >= nblocks)
         return;
-    const bool last_round = b >= prio_from;
+    const uint32_t b = order ? order[bi] : bi;       // (largest first: lzo_mi355x_launch_order_by_size)
+    const bool last_round = bi >= prio_from;
     const uint32_t l = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x == 0) {
@@ -1381,7 +1382,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         S.parsed = 0;
         S.consumed = 0;
         S.done = 0;
-        S.opset = opset_take(OpPool{pool, ring, nsets}, b);
+        S.opset = opset_take(OpPool{pool, ring, nsets}, bi);
     }
     if (threadIdx.x < kWave)
         S.flags[threadIdx.x] = 0;             // chunk tags start at 0x80000001
@@ -1841,17 +1842,63 @@ extern "C" int lzo_mi355x_launch_decompress_fast(const uint8_t* src, const uint6
                                                  uint32_t* fallback, uint32_t* fallback_ids,
                                                  uint32_t* pool, void* ring, void* ops,
                                                  uint32_t nsets, uint32_t nblocks,
-                                                 hipStream_t stream)
+                                                 uint32_t* order, hipStream_t stream)
 {
     if (nblocks == 0)
         return 0;
     if (nsets == 0)
         return -1;
+    if (order && lzo_mi355x_launch_order_by_size(dst_cap, nblocks, order, stream) != 0)
+        return -1;
     hipLaunchKernelGGL(lzo1x_decode_fast_kernel<false>, dim3(nblocks), dim3(2 * kWave), 0,
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
                        fallback, fallback_ids, (uint2*)ops, nblocks,
                        prio_from(nblocks, lzo_mi355x_fast_resident_blocks()), nullptr, pool,
-                       (unsigned long long*)ring, nsets);
+                       (unsigned long long*)ring, nsets, (const uint32_t*)order);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+namespace {
+// Counting sort of the block indices by key, largest 4 KiB class first (one
+// workgroup: class counts in LDS, their prefix sums, then each index to its
+// class's next slot; the order within a class is whatever the atomics give).
+constexpr uint32_t kOrderClasses = 256;
+__device__ __forceinline__ uint32_t order_class(uint32_t key)
+{
+    const uint32_t k = key >> 12;
+    return kOrderClasses - 1u - (k < kOrderClasses - 1u ? k : kOrderClasses - 1u);
+}
+__global__ __launch_bounds__(1024) void lzo1x_order_kernel(const uint32_t* __restrict__ key, uint32_t n,
+                                                           uint32_t* __restrict__ order)
+{
+    __shared__ uint32_t cnt[kOrderClasses];
+    const uint32_t t = threadIdx.x;
+    if (t < kOrderClasses)
+        cnt[t] = 0;
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += blockDim.x)
+        atomicAdd(&cnt[order_class(key[i])], 1u);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t sum = 0;
+        for (uint32_t c = 0; c < kOrderClasses; c++) {
+            const uint32_t v = cnt[c];
+            cnt[c] = sum;
+            sum += v;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += blockDim.x)
+        order[atomicAdd(&cnt[order_class(key[i])], 1u)] = i;
+}
+}  // namespace
+
+extern "C" int lzo_mi355x_launch_order_by_size(const uint32_t* key, uint32_t n, uint32_t* order,
+                                               hipStream_t stream)
+{
+    if (n == 0)
+        return 0;
+    hipLaunchKernelGGL(lzo1x_order_kernel, dim3(1), dim3(1024), 0, stream, key, n, order);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1870,6 +1917,6 @@ extern "C" int lzo_mi355x_debug_decompress_fast_stamps(
                        stream, src, src_off, src_len, dst, dst_off, dst_cap, out_len, status,
                        fallback, fallback_ids, (uint2*)ops, nblocks,
                        prio_from(nblocks, lzo_mi355x_fast_resident_blocks()), stamps, pool,
-                       (unsigned long long*)ring, nsets);
+                       (unsigned long long*)ring, nsets, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -82,7 +82,8 @@ constexpr uint32_t kDictBytes = (kSlots + 2) * 2 + 60;   // per workgroup, 64-by
 static_assert(kDictBytes % 64 == 0, "dictionary regions stay 64-byte aligned");
 // Scratch: [0, kScratchHead) the block ticket counter (u32, zeroed by the
 // launcher when the grid is smaller than the batch), then one dictionary
-// region per workgroup.
+// region per workgroup, then (batches of more blocks than resident
+// workgroups) the start order, u32 per block.
 constexpr uint32_t kScratchHead = 256;
 
 template <bool GD>
@@ -1042,7 +1043,7 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
-    uint8_t* __restrict__ dicts)
+    uint8_t* __restrict__ dicts, const uint32_t* __restrict__ order)
 {
     __shared__ EncLdsT<true> S;
     Dict<true> D;
@@ -1050,7 +1051,8 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
     D.g = (gu16*)(dicts + kScratchHead + (size_t)blockIdx.x * kDictBytes);
     const uint32_t l = lane_id();
     const bool dyn = nblocks > gridDim.x;
-    for (uint32_t b = blockIdx.x; b < nblocks; b = dyn ? next_block((uint32_t*)dicts) : nblocks) {
+    for (uint32_t t = blockIdx.x; t < nblocks; t = dyn ? next_block((uint32_t*)dicts) : nblocks) {
+        const uint32_t b = order ? order[t] : t;      // (largest first: lzo_mi355x_launch_order_by_size)
         const uint32_t n = src_len[b];
         if (n > kMaxN) {                             // the general encoder's
             if (l == 0)
@@ -1094,11 +1096,21 @@ static uint32_t enc_resident(void)
     return (uint32_t)cus[dev] * (enc_waves() == 1 ? POM_ENC_RESIDENT1 : POM_ENC_RESIDENT);
 }
 
+// Start order of a batch with more blocks than resident workgroups (bytes at
+// the end of the scratch, after the dictionary regions).
+static size_t enc_order_bytes(uint32_t nblocks)
+{
+    return nblocks > enc_resident() ? ((size_t)4 * nblocks + 255) / 256 * 256 : 0;
+}
+
 // Grid of the global-dictionary encoders: one workgroup per dictionary region
 // of the scratch, at most one per block and one per resident slot, and at
 // most the debug key enc_grid.
 static uint32_t enc_grid(size_t scratch_bytes, uint32_t nblocks)
 {
+    const size_t ob = enc_order_bytes(nblocks);
+    if (scratch_bytes >= kScratchHead + kDictBytes + ob)
+        scratch_bytes -= ob;                         // (room for the start order)
     uint32_t grid = scratch_bytes > kScratchHead ? (uint32_t)((scratch_bytes - kScratchHead) / kDictBytes) : 0u;
     grid = grid < nblocks ? grid : nblocks;
     grid = grid < enc_resident() ? grid : enc_resident();
@@ -1109,7 +1121,7 @@ static uint32_t enc_grid(size_t scratch_bytes, uint32_t nblocks)
 extern "C" size_t lzo_mi355x_compress_scratch(uint32_t nblocks)
 {
     const uint32_t g = nblocks < enc_resident() ? nblocks : enc_resident();
-    return kScratchHead + (size_t)g * kDictBytes;
+    return kScratchHead + (size_t)g * kDictBytes + enc_order_bytes(nblocks);
 }
 
 extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_t* src_off,
@@ -1124,9 +1136,18 @@ extern "C" int lzo_mi355x_launch_compress_fast(const uint8_t* src, const uint64_
     const uint32_t grid = scratch ? enc_grid(scratch_bytes, nblocks) : 0u;
     if (grid && grid < nblocks && hipMemsetAsync(scratch, 0, sizeof(uint32_t), stream) != hipSuccess)
         return -1;                                   // (the block ticket)
+    // largest first when the blocks outnumber the workgroups and the scratch
+    // has room for the order after the grid's dictionaries
+    const size_t ob = enc_order_bytes(nblocks);
+    const size_t order_at = kScratchHead + (size_t)grid * kDictBytes;
+    uint32_t* order = grid && grid < nblocks && ob && order_at + ob <= scratch_bytes
+                          ? (uint32_t*)((uint8_t*)scratch + order_at) : nullptr;
+    if (order && enc_waves() == 1 && lzo_mi355x_launch_order_by_size(src_len, nblocks, order, stream) != 0)
+        return -1;
     if (grid && enc_waves() == 1)
         hipLaunchKernelGGL(lzo1x_encode_gdict1_kernel, dim3(grid), dim3(kWave), 0, stream, src, src_off,
-                           src_len, dst, dst_off, dst_cap, out_len, status, nblocks, (uint8_t*)scratch);
+                           src_len, dst, dst_off, dst_cap, out_len, status, nblocks, (uint8_t*)scratch,
+                           (const uint32_t*)order);
     else if (grid)
         hipLaunchKernelGGL(lzo1x_encode_gdict_kernel<false>, dim3(grid), dim3(2 * kWave), 0, stream,
                            src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,

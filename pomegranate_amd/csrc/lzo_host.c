@@ -279,8 +279,10 @@ int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
  *   [256]   op-set pool counters (LZO_MI355X_FAST_POOL_BYTES)
  *   then    op-set return ring, u64 per set
  *   then    the fast decoder's fallback list, u32 per block
+ *   then    (more blocks than resident workgroups) the start order, u32 per block
  *   then    the op-slot sets, one per workgroup resident at once
- * Only the fallback list grows with nblocks (4 bytes a block). */
+ * Only the fallback list and the start order grow with nblocks (4 bytes a
+ * block each). */
 enum { SCR_POOL = 256, SCR_RING = SCR_POOL + LZO_MI355X_FAST_POOL_BYTES };
 
 static size_t scr_sets(uint32_t nblocks)
@@ -294,9 +296,19 @@ static size_t scr_head(uint32_t nblocks)
     return ALIGN_UP(SCR_RING + 8 * scr_sets(nblocks), 256);
 }
 
-static size_t scr_ops_off(uint32_t nblocks)
+static size_t scr_order_bytes(uint32_t nblocks)
+{
+    return nblocks > lzo_mi355x_fast_resident_blocks() ? ALIGN_UP(4 * (size_t)nblocks, 256) : 0;
+}
+
+static size_t scr_order_off(uint32_t nblocks)
 {
     return scr_head(nblocks) + ALIGN_UP(4 * (size_t)nblocks, 256);
+}
+
+static size_t scr_ops_off(uint32_t nblocks)
+{
+    return scr_order_off(nblocks) + scr_order_bytes(nblocks);
 }
 
 size_t lzo_mi355x_decompress_scratch(uint32_t nblocks)
@@ -381,7 +393,11 @@ static int decompress_dev_with(const uint8_t *src, const uint64_t *src_off, cons
         if (lzo_mi355x_launch_decompress_fast(src, src_off, src_len, dst, dst_off, dst_cap,
                                               out_len, status, fb, ids,
                                               (uint32_t *)(scr + SCR_POOL), scr + SCR_RING,
-                                              scr + scr_ops_off(nblocks), nsets, nblocks, s) != 0)
+                                              scr + scr_ops_off(nblocks), nsets, nblocks,
+                                              scr_order_bytes(nblocks)
+                                                  ? (uint32_t *)(scr + scr_order_off(nblocks))
+                                                  : NULL,
+                                              s) != 0)
             return -1;
     }
     const uint32_t ngrid = nblocks < 512 ? nblocks : 512;

@@ -47,7 +47,7 @@ fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 fast = lib.lzo_mi355x_launch_decompress_fast
 fast.restype = ctypes.c_int
-fast.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+fast.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 p = lambda x: x.data_ptr()
 sh = torch.cuda.current_stream().cuda_stream
 def run(stamp):
@@ -57,7 +57,7 @@ def run(stamp):
     if stamp:
         fn(*args, p(stamps), sh)
     else:
-        fast(*args, sh)
+        fast(*args, None, sh)
 for stamp in ((False,) if a.nostamps else (False, True)):
     run(stamp); torch.cuda.synchronize()
     ts = []

@@ -345,12 +345,13 @@ def test_fast_path_takes_every_valid_stream(dev, gu):
 def test_fast_path_op_sets_are_reused(dev, gu):
     """More blocks than workgroups resident at once: the op-slot sets are
     handed from finished workgroups to new ones (the scratch holds one set per
-    resident workgroup, not per block), every block stays on the fast path,
-    and the scratch for config C4's 131,072 blocks stays well under 300 MB."""
+    resident workgroup, not per block), the blocks start largest first (sizes
+    over four 4 KiB classes), every block stays on the fast path, and the
+    scratch for config C4's 131,072 blocks stays well under 300 MB."""
     lib = lzo.load()
     resident = int(lib.lzo_mi355x_fast_resident_blocks())
     n = 2 * resident + 123
-    blocks = [synth.block(synth.ITB, 70000 + i, 4096 + 16 * (i % 64)) for i in range(n)]
+    blocks = [synth.block(synth.ITB, 70000 + i, 256 + 2048 * (i % 8) + 16 * (i % 64)) for i in range(n)]
     comps, st = gu.gpu_compress(torch, blocks, dev)
     assert all(s == 0 for s in st)
     outs, st2, fallbacks = gu.gpu_decompress_fast(torch, comps, [len(b) for b in blocks], dev)
@@ -358,8 +359,9 @@ def test_fast_path_op_sets_are_reused(dev, gu):
     assert outs == blocks
     assert fallbacks == 0
     assert lzo.decompress_scratch_bytes(131072) < 300e6
+    # (+ the fallback list's growth, + the start order once n > resident)
     assert lzo.decompress_scratch_bytes(n) == lzo.decompress_scratch_bytes(resident) + (
-        -(-4 * n // 256) - -(-4 * resident // 256)) * 256
+        -(-4 * n // 256) - -(-4 * resident // 256)) * 256 + -(-4 * n // 256) * 256
 
 
 @pytest.mark.parametrize("nsets", [1, 3, 40])
@@ -372,7 +374,8 @@ def test_fast_path_op_set_pool_under_contention(dev, gu, nsets):
     lib = lzo.load()
     fn = lib.lzo_mi355x_launch_decompress_fast
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    fn.argtypes = [ctypes.c_void_p] * 13 + [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                            ctypes.c_void_p]
     lib.lzo_mi355x_fast_ops_bytes_per_block.restype = ctypes.c_size_t
     n = 600
     blocks = [synth.block(synth.ITB, 80000 + i, 4096 + 64 * (i % 97)) for i in range(n)]
@@ -389,7 +392,7 @@ def test_fast_path_op_set_pool_under_contention(dev, gu, nsets):
                       device=dev)
     p = lambda t: t.data_ptr()
     rc = fn(p(src.arena), p(src.off), p(src.length), p(dst.arena), p(dst.off), p(dst.length),
-            p(olen), p(ost), p(head), p(ids), p(head) + 256, p(ring), p(ops), nsets, n,
+            p(olen), p(ost), p(head), p(ids), p(head) + 256, p(ring), p(ops), nsets, n, None,
             torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
@@ -703,7 +706,9 @@ def test_small_batches_on_the_lds_encoder_vs_oracle(dev, gu, oracle, which):
 def test_encoder_block_tickets_mixed_sizes(dev, gu):
     """More blocks than the global-dictionary grid, of mixed ITB sizes (C4's
     4-256 KiB): workgroups past their first block draw the next one from the
-    ticket counter in the scratch head, whose word starts as garbage.  Every
+    ticket counter in the scratch head, whose word starts as garbage, in the
+    largest-first start order the launcher sorts into the scratch (the decode
+    back likewise, 6000 blocks being more than one resident round).  Every
     block byte-identical to the LDS-dictionary kernel (itself pinned to the
     oracle above), then decoded back."""
     n = 6000                                     # > 4096 resident on a 256-CU MI355X
