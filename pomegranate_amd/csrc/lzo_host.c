@@ -1008,8 +1008,12 @@ static int dev_run(void *arg, int d)
             }
             /* the caller's per-chunk work runs while the launched chunks' copies
              * and kernels are in flight */
-            if (done_ids && B->on_chunk)
+            if (done_ids && B->on_chunk) {
+                const double tc = g_timing ? now_ms() : 0;
                 B->on_chunk(B->cb_ctx, done_ids, done_nb);
+                if (g_timing)
+                    fprintf(stderr, "  on_chunk n=%zu: %.2f ms\n", done_nb, now_ms() - tc);
+            }
             if (!(from < nids && rc == 0)) {
                 int any = 0;
                 for (int j = 0; j < B->nslots; j++)
