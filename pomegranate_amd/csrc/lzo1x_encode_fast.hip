@@ -758,7 +758,10 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
             for (uint32_t round = 0;; round++) {
                 const bool onpath = (path >> l) & 1ull;
                 const uint32_t mine = (wtag << 8) | l;
-                atomicMin(&S.claim[onpath ? claim_index(slot) : kClaim], mine);
+                // (off-path lanes post nothing: sent to one spare entry, their
+                // atomics serialised on it -- lone 64 KiB 655 -> 640 us)
+                if (onpath)
+                    atomicMin(&S.claim[claim_index(slot)], mine);
                 wave_order();
                 const uint32_t t1 = S.claim[claim_index(h1)];
                 const uint32_t t2 = S.claim[claim_index(h2)];
@@ -850,7 +853,11 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 const uint64_t stop = ~(path & ~mstart) & below;
                 const uint32_t from = stop ? ip + 64 - (uint32_t)__builtin_clzll(stop) : ii;
                 const uint32_t r = (uint32_t)__builtin_popcountll(km & below);
-                S.tok[(km >> l) & 1ull ? (tp + r) % kTok : kTok] = make_uint4(from, p - from, mlen, p - cand);
+                // (the other lanes write nothing: sent to a spare entry, their
+                // writes to one address were serialised -- lone 64 KiB 641 -> 629
+                // us, with the dictionary put below)
+                if ((km >> l) & 1ull)
+                    S.tok[(tp + r) % kTok] = make_uint4(from, p - from, mlen, p - cand);
                 tp += cnt;
                 lds_store(&S.prod, tp);
                 const uint32_t last = 63 - (uint32_t)__builtin_clzll(km);
@@ -864,7 +871,8 @@ __device__ void parse_wave(EncLdsT<GD>& S, const Dict<GD> D, const uint8_t* in, 
                 if ((path & keep & ~superseded) >> l & 1ull)
                     D.put(slot, p - base + 1);
             } else {
-                D.put((path & keep & ~superseded) >> l & 1ull ? slot : kSlots, p - base + 1);
+                if ((path & keep & ~superseded) >> l & 1ull)
+                    D.put(slot, p - base + 1);
             }
             wave_order();
             ESTAMP(EP_DICT);
