@@ -43,8 +43,10 @@ void lzo_mi355x_debug_reload(void);
 /* `scratch`: device memory of lzo_mi355x_compress_scratch(nblocks) bytes for
  * the per-workgroup match dictionaries (32 KiB each; 16 blocks per CU are then
  * parsed at once) after a 256-byte head (the block ticket of batches larger
- * than the grid, reset by the call on `stream`), or NULL (dictionaries in LDS:
- * 4 blocks per CU).  No initial contents are required. */
+ * than the grid, reset by the call on `stream`), then, for batches of more
+ * blocks than resident workgroups, 4 bytes a block for the start order
+ * (largest blocks first, sorted by the call on `stream`); or NULL
+ * (dictionaries in LDS: 4 blocks per CU).  No initial contents are required. */
 int lzo_mi355x_compress_dev(const uint8_t *src, const uint64_t *src_off,
                             const uint32_t *src_len, uint8_t *dst,
                             const uint64_t *dst_off, const uint32_t *dst_cap,
@@ -57,7 +59,8 @@ size_t lzo_mi355x_compress_scratch(uint32_t nblocks);
  * bytes for nblocks, or NULL (every block then takes the exact one-wave
  * decoder).  The scratch holds a 4-byte-a-block list plus op slots for the
  * workgroups resident at once (not per block): about 100 MB plus 4 bytes a
- * block.  After the call, the u32 at scratch byte 0 counts the blocks the
+ * block (8 for batches of more blocks than resident workgroups: their start
+ * order, largest first, sorted by the call on `stream`).  After the call, the u32 at scratch byte 0 counts the blocks the
  * throughput decoder handed to the exact (one wave per block, ~20x slower)
  * decoder: malformed streams, capacity or look-behind errors, destinations not
  * 16-byte aligned (the windowed decoder, which small batches take, needs only
