@@ -88,8 +88,10 @@ constexpr uint32_t kScratchHead = 256;
 
 template <bool GD>
 struct __attribute__((aligned(16))) EncLdsT {
-    // (each array has one spare entry past its end: the target of the writes
-    // of lanes that take no part, instead of an exec-masked branch)
+    // (the spare entry past the end of dict, claim and tok took the writes of
+    // lanes with no part in them until round 5; those writes are exec-masked
+    // now -- 50-odd lanes writing one LDS address serialised -- and the
+    // entries stay only to keep the measured layout)
     uint16_t dict[GD ? 2 : kSlots + 2]; // last probe position per hash slot: position - base + 1 (0 = empty)
     uint32_t claim[kClaim + 1];     // (window tag << 8 | lowest writing lane) per hashed slot
     uint4 tok[kTok + 1];            // {literal start, literal count, match length (0: tail), offset}
