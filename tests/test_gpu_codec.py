@@ -342,6 +342,28 @@ def test_fast_path_takes_every_valid_stream(dev, gu):
     assert fallbacks == 0
 
 
+def test_start_order_is_largest_first(dev):
+    """lzo_mi355x_launch_order_by_size (the start order of batches larger than
+    one resident round): a permutation of the block indices whose 4 KiB size
+    classes never increase, every size above 1 MiB in the first class."""
+    lib = lzo.load()
+    fn = lib.lzo_mi355x_launch_order_by_size
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(11)
+    for n in (1, 1023, 10000):
+        keys = rng.integers(0, 3 << 20, n).astype(np.uint32)
+        keys[: n // 7] = rng.integers(0, 8192, n // 7)          # (many small ones)
+        kd = torch.from_numpy(keys.view(np.int32)).to(dev)
+        order = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        assert fn(kd.data_ptr(), n, order.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        o = order.cpu().numpy().astype(np.int64)
+        assert sorted(o.tolist()) == list(range(n))
+        cls = np.minimum(keys[o] >> 12, 255)
+        assert (np.diff(cls.astype(np.int64)) <= 0).all()
+
+
 def test_fast_path_op_sets_are_reused(dev, gu):
     """More blocks than workgroups resident at once: the op-slot sets are
     handed from finished workgroups to new ones (the scratch holds one set per
