@@ -174,6 +174,8 @@ def cpu_c1(synth, seconds):
         lib.lzo1x_1_compress(p_, len(p_), z, ctypes.byref(zl), wrk)
         comps.append(z.raw[: zl.value])
     j = _cpu_bench(plain, comps, threads, seconds)
+    if j is None:                                   # oracle/cpu_bench not built
+        return None
     leg = _leg(j)
     return {"roundtrip_value": leg["value"], "unit": "GiB/s", "cores": threads,
             "compress_value": leg["compress_value"], "decompress_value": leg["decompress_value"],
@@ -886,22 +888,60 @@ def run_others(args, torch, dist, lzo, synth, shard, dev, world, rank, backend):
     return out
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N rank
+    processes through torch.distributed.run on 127.0.0.1 -- one per GPU, the
+    driver's own command -- and return their exit code.  Runs before anything
+    imports torch or touches a GPU (the ranks are children, not an exec)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    print(f"bench: --gpus {n} without a launcher: starting {n} ranks", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
+def rank_plan(args):
+    """(world, rank, local rank) from the launcher's environment.  A request
+    for N GPUs is never measured on a different number of ranks: a WORLD_SIZE
+    that disagrees with --gpus is an error."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus={args.gpus}; "
+                         "the run must have one rank per requested GPU")
+    return world, rank, local
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be at least 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus))
+    world, rank, local = rank_plan(args)
+    if os.environ.get("POM_BENCH_PLAN_ONLY"):
+        # (tests: the rank layout a run would use, without touching a GPU)
+        print(json.dumps({"plan": True, "n_gpus": world, "rank": rank, "local_rank": local}),
+              flush=True)
+        return
     import torch
     import torch.distributed as dist
 
     from pomegranate_amd import lzo, shard, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}", file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the LZO1X path has no CPU fallback)")
     # One process per GPU.  POM_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs.
     backend = os.environ.get("POM_DIST_BACKEND", "nccl")
+    if backend == "nccl" and world > torch.cuda.device_count():
+        raise SystemExit(f"bench: {world} ranks over RCCL need {world} GPUs, "
+                         f"{torch.cuda.device_count()} visible")
     dev = torch.device(f"cuda:{local % torch.cuda.device_count()}")
     torch.cuda.set_device(dev)
     # One rank per GPU: the library's host batches stay on this rank's GPU

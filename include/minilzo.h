@@ -78,12 +78,16 @@ typedef union {
 #define LZO_E_INPUT_NOT_CONSUMED (-8)
 #define LZO_E_NOT_YET_IMPLEMENTED (-9)
 
-/* Work-memory sizes, lib/minilzo.h:80-81.  Callers allocate this much
+/* Work-memory sizes, lib/minilzo.h:79-81.  Callers allocate this much
  * (mds/txg.c:835, api/api.c:1140); the GPU codec does not read it: output is
  * defined as the reference's output with a zero-filled wrkmem. */
 #define lzo_sizeof_dict_t ((unsigned)sizeof(lzo_bytep))
 #define LZO1X_1_MEM_COMPRESS ((lzo_uint32)(16384L * lzo_sizeof_dict_t))
+#define LZO1X_MEM_COMPRESS LZO1X_1_MEM_COMPRESS
 #define LZO1X_MEM_DECOMPRESS (0)
+
+/* Pointer-sized unsigned integer (lib/lzoconf.h:198-222 on LP64). */
+typedef unsigned long lzo_uintptr_t;
 
 /* Replaces lib/minilzo.c:2567-2598 (__lzo_init_v2).  Checks the caller's
  * type sizes like the reference, then that a gfx950 GPU is usable. */
@@ -93,10 +97,32 @@ int __lzo_init_v2(unsigned, int, int, int, int, int, int, int, int, int);
                   (int)sizeof(lzo_uint32), (int)sizeof(lzo_uint), (int)lzo_sizeof_dict_t, \
                   (int)sizeof(char *), (int)sizeof(lzo_voidp), (int)sizeof(lzo_callback_t))
 
-/* Replaces lib/minilzo.c:2404-2420. */
+/* Version functions: replace lib/minilzo.c:2306-2344 (declared at
+ * lib/lzoconf.h:338-342). */
 unsigned lzo_version(void);
 const char *lzo_version_string(void);
 const char *lzo_version_date(void);
+/* (the reference declares these `const lzo_charp` / `const lzo_bytep`: a
+ * top-level const on a return type, which C ignores; the type is the same) */
+lzo_charp _lzo_version_string(void);
+lzo_charp _lzo_version_date(void);
+lzo_bytep lzo_copyright(void);
+
+/* Host utilities the reference's minilzo.c also exports (lib/lzoconf.h:344-372).
+ * They touch no compressed data and run on the host, as in the reference. */
+int lzo_memcmp(const lzo_voidp a, const lzo_voidp b, lzo_uint len);   /* lib/minilzo.c:2421 */
+lzo_voidp lzo_memcpy(lzo_voidp dst, const lzo_voidp src, lzo_uint len);
+lzo_voidp lzo_memmove(lzo_voidp dst, const lzo_voidp src, lzo_uint len);
+lzo_voidp lzo_memset(lzo_voidp buf, int c, lzo_uint len);
+/* Adler-32 with the reference's buf == NULL -> 1 rule (lib/minilzo.c:2355-2391). */
+lzo_uint32 lzo_adler32(lzo_uint32 c, const lzo_bytep buf, lzo_uint len);
+/* lib/minilzo.c:2522-2561: LZO_E_OK when the byte order and unaligned access
+ * the library assumes hold. */
+int _lzo_config_check(void);
+/* lib/minilzo.c:2251-2287. */
+lzo_uintptr_t __lzo_ptr_linear(const lzo_voidp ptr);
+unsigned __lzo_align_gap(const lzo_voidp p, lzo_uint size);
+#define LZO_PTR_ALIGN_UP(p, size) ((p) + (lzo_uint)__lzo_align_gap((const lzo_voidp)(p), (lzo_uint)(size)))
 
 /* Replaces lib/minilzo.c:3159-3207 (lzo1x_1_compress).  Output is
  * byte-identical to the reference with a zero-filled wrkmem; dst must hold

@@ -92,9 +92,13 @@ int pom_abuf_close(struct pom_abuf *ab);
  * same batch can lay the file out differently (readers go by locations[];
  * the debug key ooo=0 delivers chunks in launch order, largest blocks first).
  * Returns 0, LZO_E_ERROR when the GPU path is unusable, or the first append's
- * -errno; on any failure the append point is put back where it was on entry
- * (nothing of the batch stays appended) and every locations[b] is UINT64_MAX,
- * so the caller may retry the whole batch. */
+ * -errno; on any failure the append point is put back where it was on entry,
+ * the bytes the batch's appends had written past it are zeroed, and every
+ * locations[b] is UINT64_MAX, so the caller may retry the whole batch.  If the
+ * append point's window cannot be mapped again, it returns POM_ABUF_E_BROKEN:
+ * the abuf then refuses appends, and pom_abuf_close still cuts the file at
+ * the append point of entry. */
+#define POM_ABUF_E_BROKEN (-4096)
 int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, const size_t *tmp_cap,
                                       uint8_t **oi, int *err, size_t n, struct pom_abuf *ab,
                                       uint64_t *locations);

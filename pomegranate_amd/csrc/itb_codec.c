@@ -242,23 +242,46 @@ int pom_itb_lzo_compress_batch(uint8_t *const *in, uint8_t *const *tmp, const si
 
 static int abuf_map(struct pom_abuf *ab);
 
-/* Puts the append point back to (file_offset, offset): the window holding it
- * is mapped again if the appends moved on to later windows.  What was written
- * past it is overwritten by the next appends and cut off at close. */
+/* Puts the append point back to (file_offset, offset) and zeroes what the
+ * rolled-back appends wrote past it, so neither a reader nor a crash before
+ * close finds a record of the failed batch.  The bookkeeping is restored
+ * first: even when the window cannot be mapped again, pom_abuf_close
+ * truncates at the restored point.  A failed munmap or remap leaves addr
+ * NULL (the abuf refuses appends) and returns -errno. */
 static int abuf_rollback(struct pom_abuf *ab, uint64_t file_offset, size_t offset, uint64_t acclen)
 {
-    if (ab->file_offset != file_offset || !ab->addr) {
+    const uint64_t reached = ab->file_offset + ab->offset, at = file_offset + offset;
+    int rc = 0;
+    const int remap = ab->file_offset != file_offset || !ab->addr;
+    if (remap) {
         if (ab->addr && munmap(ab->addr, ab->win) != 0)
-            return -errno;
+            rc = -errno;
         ab->addr = NULL;
-        ab->file_offset = file_offset;
-        const int rc = abuf_map(ab);
-        if (rc)
-            return rc;
     }
+    ab->file_offset = file_offset;
     ab->offset = offset;
     ab->acclen = acclen;
-    return 0;
+    if (reached > at &&
+        fallocate(ab->fd, FALLOC_FL_PUNCH_HOLE | FALLOC_FL_KEEP_SIZE, (off_t)at, (off_t)(reached - at)) != 0) {
+        static const uint8_t zeros[1 << 16];
+        for (uint64_t o = at; o < reached && !rc;) {
+            const size_t w = reached - o < sizeof zeros ? (size_t)(reached - o) : sizeof zeros;
+            const ssize_t k = pwrite(ab->fd, zeros, w, (off_t)o);
+            if (k <= 0)
+                rc = k < 0 ? -errno : -EIO;
+            else
+                o += (uint64_t)k;
+        }
+    }
+    if (remap && !rc) {
+        rc = pom_dbg_int("fail_remap", 0) ? -ENOMEM : abuf_map(ab);   /* (debug key: tests) */
+        ab->offset = offset;                       /* abuf_map starts a window at 0 */
+        if (rc && ab->addr) {
+            munmap(ab->addr, ab->win);
+            ab->addr = NULL;
+        }
+    }
+    return rc;
 }
 
 /* Page-cache pages for a batch's appends, allocated ahead by a helper thread
@@ -340,8 +363,8 @@ int pom_itb_lzo_compress_append_batch(uint8_t *const *in, uint8_t *const *tmp, c
         const int rb = abuf_rollback(ab, fo0, off0, acc0);
         for (size_t b = 0; b < n; b++)
             locations[b] = UINT64_MAX;
-        if (rb && rc == LZO_E_OK)
-            rc = rb;
+        if (rb)
+            rc = POM_ABUF_E_BROKEN;                /* the caller must know the abuf is unusable */
     }
     pthread_mutex_destroy(&w.mu);
     itb_wb_free(&w, n);

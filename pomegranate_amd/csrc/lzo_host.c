@@ -34,31 +34,39 @@
  * sc_trace=1, host_timing=1, slots=N, chunk_mb=N, dec_small_first=0, ooo=0, enc_lds_max=N, enc_waves=1|2,
  * enc_grid=N, fail_chunk=K (tests: a device's K-th chunk delivery fails).  The variable is read once, at the first use, into a private
  * copy; lzo_mi355x_debug_reload() reads it again (tests change it between
- * calls).  So the hot paths never call getenv, and a concurrent setenv cannot
- * race with a lookup. */
+ * calls).  So the hot paths never call getenv.  Each (re)load publishes a new,
+ * immutable copy through one atomic pointer, so a lookup on any thread reads
+ * either the old or the new string whole, never one being rewritten (ADVICE
+ * r5); the replaced copies are not freed (a reload is a test-time event and a
+ * lookup may still be reading one). */
 static pthread_mutex_t dbg_mu = PTHREAD_MUTEX_INITIALIZER;
-static char dbg_val[512];
-static int dbg_loaded;
+static const char *dbg_cur;
+
+static void dbg_load(int always)
+{
+    pthread_mutex_lock(&dbg_mu);
+    if (always || !dbg_cur) {
+        const char *e = getenv("POM_LZO_DEBUG");
+        char *copy = strdup(e ? e : "");
+        if (copy)
+            __atomic_store_n(&dbg_cur, copy, __ATOMIC_RELEASE);
+    }
+    pthread_mutex_unlock(&dbg_mu);
+}
 
 void lzo_mi355x_debug_reload(void)
 {
-    pthread_mutex_lock(&dbg_mu);
-    const char *e = getenv("POM_LZO_DEBUG");
-    size_t n = e ? strlen(e) : 0;
-    if (n >= sizeof dbg_val)
-        n = sizeof dbg_val - 1;
-    memcpy(dbg_val, e ? e : "", n);
-    dbg_val[n] = 0;
-    __atomic_store_n(&dbg_loaded, 1, __ATOMIC_RELEASE);
-    pthread_mutex_unlock(&dbg_mu);
+    dbg_load(1);
 }
 
 const char *pom_dbg_str(const char *key, char *buf, size_t n)
 {
-    if (!__atomic_load_n(&dbg_loaded, __ATOMIC_ACQUIRE))
-        lzo_mi355x_debug_reload();
-    const char *e = dbg_val;
-    if (!*e || !n)
+    const char *e = __atomic_load_n(&dbg_cur, __ATOMIC_ACQUIRE);
+    if (!e) {
+        dbg_load(0);                              /* first use */
+        e = __atomic_load_n(&dbg_cur, __ATOMIC_ACQUIRE);
+    }
+    if (!e || !*e || !n)
         return NULL;
     const size_t kl = strlen(key);
     for (const char *p = e; *p;) {
@@ -1202,6 +1210,58 @@ int __lzo_init_v2(unsigned v, int s1, int s2, int s3, int s4, int s5, int s6, in
 unsigned lzo_version(void) { return LZO_VERSION; }
 const char *lzo_version_string(void) { return LZO_VERSION_STRING; }
 const char *lzo_version_date(void) { return LZO_VERSION_DATE; }
+lzo_charp _lzo_version_string(void) { return (lzo_charp)LZO_VERSION_STRING; }
+lzo_charp _lzo_version_date(void) { return (lzo_charp)LZO_VERSION_DATE; }
+/* lib/minilzo.c:2306-2314 (minilzo builds return LZO_VERSION_STRING) */
+lzo_bytep lzo_copyright(void) { return (lzo_bytep)LZO_VERSION_STRING; }
+
+/* Host utilities of the reference's minilzo.c (lib/minilzo.c:2355-2500). */
+int lzo_memcmp(const lzo_voidp a, const lzo_voidp b, lzo_uint len) { return memcmp(a, b, len); }
+lzo_voidp lzo_memcpy(lzo_voidp dst, const lzo_voidp src, lzo_uint len) { return memcpy(dst, src, len); }
+lzo_voidp lzo_memmove(lzo_voidp dst, const lzo_voidp src, lzo_uint len) { return memmove(dst, src, len); }
+lzo_voidp lzo_memset(lzo_voidp buf, int c, lzo_uint len) { return memset(buf, c, len); }
+
+lzo_uint32 lzo_adler32(lzo_uint32 c, const lzo_bytep buf, lzo_uint len)
+{
+    if (buf == NULL)
+        return 1;
+    uint32_t lo = c & 0xffffu, hi = (c >> 16) & 0xffffu;
+    const unsigned char *p = buf;
+    while (len > 0) {
+        /* 5552 bytes keep both sums below 2^32 before the reduction */
+        lzo_uint k = len < 5552 ? len : 5552;
+        len -= k;
+        for (lzo_uint i = 0; i < k; i++) {
+            lo += p[i];
+            hi += lo;
+        }
+        p += k;
+        lo %= 65521u;
+        hi %= 65521u;
+    }
+    return (hi << 16) | lo;
+}
+
+int _lzo_config_check(void)
+{
+    union {
+        unsigned long a[2];
+        unsigned char b[2 * sizeof(unsigned long)];
+    } u;
+    u.a[0] = u.a[1] = 0;
+    u.b[0] = 128;
+    lzo_uint v;
+    memcpy(&v, u.b, sizeof v);
+    return v == 128 ? LZO_E_OK : LZO_E_ERROR;       /* little-endian, as the codec assumes */
+}
+
+lzo_uintptr_t __lzo_ptr_linear(const lzo_voidp ptr) { return (lzo_uintptr_t)ptr; }
+
+unsigned __lzo_align_gap(const lzo_voidp p, lzo_uint size)
+{
+    const lzo_uintptr_t a = (lzo_uintptr_t)p;
+    return size ? (unsigned)(((a + size - 1) / size) * size - a) : 0u;
+}
 
 /* ---- single calls ------------------------------------------------------------
  * The minilzo.h entry points code one block per call, synchronously.  Calls

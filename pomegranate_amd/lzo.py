@@ -40,6 +40,9 @@ LZO_VERSION = 0x2040
 # Exported symbols, exactly those declared in include/*.h.
 EXPORTS = (
     "__lzo_init_v2", "lzo_version", "lzo_version_string", "lzo_version_date",
+    "_lzo_version_string", "_lzo_version_date", "lzo_copyright",
+    "lzo_memcmp", "lzo_memcpy", "lzo_memmove", "lzo_memset", "lzo_adler32",
+    "_lzo_config_check", "__lzo_ptr_linear", "__lzo_align_gap",
     "lzo1x_1_compress", "lzo1x_decompress", "lzo1x_decompress_safe",
     "lzo_mi355x_worst_compress", "lzo_mi355x_device_count", "lzo_mi355x_debug_reload",
     "lzo_mi355x_decoded_length",

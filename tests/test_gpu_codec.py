@@ -916,6 +916,17 @@ def test_latency_decoder_zero_runs_stay_linear(dev, oracle):
     for d in (bytes(8 << 20), synth.block(synth.ITB, 71, 65536) + bytes(4 << 20) + synth.block(synth.ITB, 72, 65536)):
         cases.append((oracle.compress(d), len(d)))
     lzo.lzo1x_decompress_safe(cases[1][0], cases[1][1])     # (warm: staging, code objects)
+    # the same call on an ITB stream of the largest output size, no zero run:
+    # the scale the zero-run cases are held to (a shared box's host and GPU
+    # load move both alike; an O(z^2) scan takes seconds)
+    itb8 = synth.block(synth.ITB, 73, 8 << 20)
+    zi = oracle.compress(itb8)
+    lzo.lzo1x_decompress_safe(zi, len(itb8))
+    t0 = time.perf_counter()
+    rc, out = lzo.lzo1x_decompress_safe(zi, len(itb8))
+    base = time.perf_counter() - t0
+    assert rc == 0 and out == itb8
+    print(f"ITB 8 MiB reference call: {base * 1e3:.1f} ms")
     for z, cap in cases:
         t0 = time.perf_counter()
         rc, out = lzo.lzo1x_decompress_safe(z, cap)
@@ -923,7 +934,7 @@ def test_latency_decoder_zero_runs_stay_linear(dev, oracle):
         print(f"zero-run case: {len(z)} B in, rc={rc}, {dt * 1e3:.1f} ms")
         want = oracle.decompress_safe(z, cap)
         assert (rc, out) == want
-        assert dt < 0.1, dt
+        assert dt < max(1.0, 10 * base), (dt, base)
 
 
 @pytest.mark.parametrize("k", [1, 3, 8])

@@ -287,6 +287,10 @@ def test_append_batch_failure_leaves_the_file_as_it_was(tmp_path, monkeypatch):
     lzo.debug_reload()
     with pytest.raises(RuntimeError):
         itb.compress_append_batch(recs, tmps, af)
+    lead_bytes = sum(itb.header_fields(r)[0] for r in first)
+    with open(path, "rb") as f:                            # the failed batch's bytes are gone
+        f.seek(lead_bytes)
+        assert not any(f.read())
     monkeypatch.setenv("POM_LZO_DEBUG", "chunk_mb=1")
     lzo.debug_reload()
     which, err, locs = itb.compress_append_batch(recs, tmps, af)
@@ -294,12 +298,46 @@ def test_append_batch_failure_leaves_the_file_as_it_was(tmp_path, monkeypatch):
     assert err == [0] * len(recs)
     sent = [t if w else r for r, t, w in zip(recs, tmps, which)]
     lens = [itb.header_fields(o)[0] for o in sent]
-    lead_bytes = sum(itb.header_fields(r)[0] for r in first)
     assert os.path.getsize(path) == lead_bytes + sum(lens)
     assert min(locs) == lead_bytes
     fd = os.open(path, os.O_RDONLY)
     try:
         for loc, r in list(zip(lead, first)) + list(zip(locs, sent)):
+            ln = itb.header_fields(r)[0]
+            assert bytes(itb.read_record(fd, loc)[:ln]) == bytes(r[:ln])
+    finally:
+        os.close(fd)
+
+
+@pytest.mark.gpu
+def test_append_batch_rollback_remap_failure(tmp_path, monkeypatch):
+    """when the rollback cannot map the append point's window
+    again (debug key fail_remap), the call says so (POM_ABUF_E_BROKEN), the
+    abuf refuses further appends, and close still cuts the file at the append
+    point of entry -- the records appended before the batch stay whole."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    first = _records(5, seed=41)
+    recs = _records(50, seed=42)
+    tmps = [bytearray(itb.ITB_FULL) for _ in recs]
+    path = str(tmp_path / "broken.itb")
+    af = itb.AppendFile(path, win=1 << 16)                 # small windows: the batch crosses several
+    lead = af.append_batch(first, [itb.header_fields(r)[0] for r in first])
+    lead_bytes = sum(itb.header_fields(r)[0] for r in first)
+    monkeypatch.setenv("POM_LZO_DEBUG", "chunk_mb=1,fail_chunk=2,fail_remap=1")
+    lzo.debug_reload()
+    with pytest.raises(RuntimeError, match="-4096"):
+        itb.compress_append_batch(recs, tmps, af)
+    monkeypatch.setenv("POM_LZO_DEBUG", "")
+    lzo.debug_reload()
+    with pytest.raises(OSError):
+        af.append_batch(first[:1], [itb.header_fields(first[0])[0]])
+    af.close()
+    assert os.path.getsize(path) == lead_bytes
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        for loc, r in zip(lead, first):
             ln = itb.header_fields(r)[0]
             assert bytes(itb.read_record(fd, loc)[:ln]) == bytes(r[:ln])
     finally:

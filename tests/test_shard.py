@@ -194,3 +194,38 @@ def test_rccl_world_one_barrier_and_c4_share():
     assert barrier == (3, 1.25)
     assert errors == 0 and nblocks == 256 and value > 0
     assert p.exitcode == 0
+
+
+def _bench(args, env_extra, timeout=240):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_gpus_n_without_launcher_starts_n_ranks():
+    """`bench.py --gpus 2` with no WORLD_SIZE starts two
+    rank processes itself (torch.distributed.run on 127.0.0.1) instead of
+    measuring one GPU; each rank sees world size 2."""
+    import json
+    r = _bench(["--gpus", "2"], {"POM_DIST_BACKEND": "gloo", "POM_BENCH_PLAN_ONLY": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    plans = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(p["rank"] for p in plans) == [0, 1]
+    assert all(p["n_gpus"] == 2 for p in plans)
+
+
+def test_bench_gpus_n_never_reports_one_gpu():
+    """Without a GPU the ranks fail, and so does the whole run: no one-GPU
+    JSON line for a two-GPU request; a WORLD_SIZE that disagrees with --gpus
+    is refused."""
+    r = _bench(["--gpus", "2"], {"POM_DIST_BACKEND": "gloo"})
+    assert r.returncode != 0
+    assert '"n_gpus": 1' not in r.stdout
+    r = _bench(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0",
+                                 "POM_BENCH_PLAN_ONLY": "1"}, timeout=60)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
