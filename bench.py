@@ -118,9 +118,12 @@ def _ref_lib():
     return lib
 
 
-def _cpu_bench(plain, comps, threads, seconds):
+def _cpu_bench(plain, comps, threads, seconds, wrk="reuse"):
     """oracle/cpu_bench (native pthreads, no Python in the loop) on the sample:
-    lib/minilzo.c from oracle/_ref, else the oracle port.  Returns its JSON."""
+    lib/minilzo.c from oracle/_ref, else the oracle port.  Returns its JSON.
+    This process keeps to one CPU of its set while the harness runs, and the
+    harness's threads avoid that CPU (POM_CPU_AVOID) while they are fewer than
+    the set."""
     import struct
     import subprocess
     import tempfile
@@ -138,9 +141,21 @@ def _cpu_bench(plain, comps, threads, seconds):
             f.write(p_)
             f.write(z_)
     try:
-        r = subprocess.run([exe, lib, path, str(threads), str(seconds)], capture_output=True,
-                           text=True, timeout=seconds + 120)
+        full = os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        full = None
+    env = dict(os.environ)
+    if full and len(full) > 1:
+        mine = max(full)
+        env["POM_CPU_AVOID"] = str(mine)
+        os.sched_setaffinity(0, {mine})
+    try:
+        r = subprocess.run([exe, lib, path, str(threads), str(seconds), "1", wrk], capture_output=True,
+                           text=True, timeout=seconds + 120, env=env,
+                           preexec_fn=(lambda: os.sched_setaffinity(0, full)) if full else None)
     finally:
+        if full:
+            os.sched_setaffinity(0, full)
         os.unlink(path)
     if r.returncode != 0:
         raise RuntimeError(f"cpu_bench failed ({r.returncode}): {r.stderr.strip()[:200]}")
@@ -206,13 +221,35 @@ def cpu_baseline(plain, comps, seconds, roundtrip=True):
     by = {str(c): _leg(j, roundtrip) for c, j in runs.items()}
     top, one = by[str(share)], by["1"]
     j = runs[share]
+    # One core in the two other regimes, so the one-core figure can be set
+    # against the single-call one (lib/minilzo.c on one 64 KiB block, the
+    # wrkmem zeroed per call): the same cycled sample with the wrkmem zeroed
+    # before every call, and one block repeated (cache-resident) likewise.
+    one_zero = _cpu_bench(plain, comps, 1, seconds / 2, wrk="zero")
+    one_res = _cpu_bench(plain[:1], comps[:1], 1, seconds / 2, wrk="zero")
+    regimes = {
+        "cycled_reused_wrkmem": {"compress_value": one["compress_value"],
+                                 "decompress_value": one["decompress_value"],
+                                 "working_set_bytes": runs[1]["per_thread_working_set_bytes"]},
+        "cycled_zeroed_wrkmem": {"compress_value": _leg(one_zero)["compress_value"],
+                                 "decompress_value": _leg(one_zero)["decompress_value"],
+                                 "working_set_bytes": one_zero["per_thread_working_set_bytes"]},
+        "resident_zeroed_wrkmem": {"compress_value": _leg(one_res)["compress_value"],
+                                   "decompress_value": _leg(one_res)["decompress_value"],
+                                   "working_set_bytes": one_res["per_thread_working_set_bytes"]},
+        "note": ("one_core (and value) reuse each thread's wrkmem across calls without clearing "
+                 "it, as mds/itb.c:2913 does, and cycle the whole sample: the dictionary then "
+                 "holds the previous blocks' pointers, and lzo1x_1_compress runs slower than "
+                 "on a zeroed wrkmem; the single-call figure (other_configs.single ... ref) "
+                 "zeroes the wrkmem and repeats one cache-resident block, the "
+                 "resident_zeroed_wrkmem regime here")}
     return {"value": top["value"], "unit": "GiB/s", "cores": share,
             "affinity_cpus": affinity_cpus(), "host": host_cpu_info(),
             "kind": j["kind"], "compress_value": top["compress_value"],
             "decompress_value": top["decompress_value"],
             "scaling_vs_one_core": {"compress": round(top["compress_value"] / one["compress_value"], 2),
                                     "decompress": round(top["decompress_value"] / one["decompress_value"], 2)},
-            "by_threads": by, "one_core": one,
+            "by_threads": by, "one_core": one, "one_core_regimes": regimes,
             "byte_identical_blocks": f"{j['byte_identical']}/{j['blocks']}",
             "harness": "oracle/cpu_bench.c (pthreads, pinned, wrkmem reused per thread as mds/itb.c:2913)",
             "sample": f"{len(plain)} of the same {len(plain[0])}-byte ITB blocks, round-robin over "

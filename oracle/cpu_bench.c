@@ -6,7 +6,7 @@
  * the reference was not built, the oracle port (oracle/liboracle.so) -- on a
  * fixed number of host threads with no Python in the loop:
  *
- *   cpu_bench LIB SAMPLE THREADS SECONDS [PIN]
+ *   cpu_bench LIB SAMPLE THREADS SECONDS [PIN] [WRK]
  *
  * SAMPLE holds the blocks: u32 count, then per block u32 n, u32 z, n plain
  * bytes, z compressed bytes (bench.py writes it from the GPU's own batch).
@@ -17,8 +17,13 @@
  * the unchecked decoder Pomegranate's callers use: mds/itb.c:2964,
  * mdsl/gc.c:770) for 0.6 * SECONDS, phase 2 compresses (lzo1x_1_compress,
  * mds/itb.c:2923) for 0.4 * SECONDS, both threads started together behind a
- * barrier.  As in mds/itb.c:2913, a thread reuses its wrkmem across calls
- * without clearing it.  Before timing, every block is checked: decompress
+ * barrier.  WRK "reuse" (the default): as in mds/itb.c:2913, a thread reuses
+ * its wrkmem across calls without clearing it, so the dictionary holds the
+ * previous blocks' positions; "zero": the wrkmem is zeroed before every call
+ * (inside the timed loop, as a caller that wants the defined output would).
+ * Environment POM_CPU_AVOID=c: CPU c (the launching process's) takes no
+ * thread while the threads are fewer than the affinity set.
+ * Before timing, every block is checked: decompress
  * gives the plain bytes, and compress with a zero-filled wrkmem gives exactly
  * the compressed bytes of the sample (the GPU's -- C3 byte identity).
  *
@@ -88,7 +93,7 @@ struct thr {
     double dec_bytes, dec_time, comp_bytes, comp_time;
     int errors;
 };
-static int nthreads;
+static int nthreads, zero_wrk;
 
 static void *worker(void *arg)
 {
@@ -122,6 +127,8 @@ static void *worker(void *arg)
     b = (uint32_t)t->index % nblocks;
     while (t1 < end) {
         size_t ol;
+        if (zero_wrk)
+            memset(wrk, 0, WRKMEM);
         int rc = do_compress(blocks[b].plain, blocks[b].n, out, &ol, wrk);
         t->errors += rc != 0;
         bytes += blocks[b].n;
@@ -156,7 +163,8 @@ static uint8_t *slurp(const char *path, size_t *len)
 int main(int argc, char **argv)
 {
     if (argc < 5) {
-        fprintf(stderr, "usage: %s LIB SAMPLE THREADS SECONDS [PIN: 1|0|spread]\n", argv[0]);
+        fprintf(stderr, "usage: %s LIB SAMPLE THREADS SECONDS [PIN: 1|0|spread] [WRK: reuse|zero]\n",
+                argv[0]);
         return 2;
     }
     void *lib = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
@@ -233,13 +241,18 @@ int main(int argc, char **argv)
      * pinning (the scheduler places the threads), "spread" thread t on CPU
      * t * (affinity set / threads) of the set */
     const char *pin = argc > 5 ? argv[5] : "1";
+    zero_wrk = argc > 6 && strcmp(argv[6], "zero") == 0;
+    const int nthr_arg = atoi(argv[3]) > 0 ? atoi(argv[3]) : 1;
+    const char *avoid_s = getenv("POM_CPU_AVOID");
+    const int avoid = avoid_s && *avoid_s ? atoi(avoid_s) : -1;
     cpu_set_t aff;
-    int cpus[CPU_SETSIZE], naff = 0;
+    int cpus[CPU_SETSIZE], naff = 0, nset = 0;
     if (sched_getaffinity(0, sizeof(aff), &aff) == 0)
         for (int c = 0; c < CPU_SETSIZE; c++)
-            if (CPU_ISSET(c, &aff))
-                cpus[naff++] = c;
-    const int nthr_arg = atoi(argv[3]) > 0 ? atoi(argv[3]) : 1;
+            nset += CPU_ISSET(c, &aff) ? 1 : 0;
+    for (int c = 0; c < CPU_SETSIZE; c++)
+        if (CPU_ISSET(c, &aff) && !(c == avoid && nthr_arg < nset))
+            cpus[naff++] = c;
     const int stride = strcmp(pin, "spread") == 0 && naff > nthr_arg ? naff / nthr_arg : 1;
     if (strcmp(pin, "0") == 0)
         naff = 0;
@@ -264,7 +277,14 @@ int main(int argc, char **argv)
         ct = T[i].comp_time > ct ? T[i].comp_time : ct;
         errors += T[i].errors;
     }
-    printf("{\"kind\": \"%s\", \"threads\": %d, \"affinity_cpus\": %d, \"pin\": \"%s\", \"blocks\": %u, "
+    double sample_bytes = 0;
+    for (uint32_t i = 0; i < nblocks; i++)
+        sample_bytes += (double)blocks[i].n + blocks[i].z;
+    const uint32_t per_thr = (nblocks + (uint32_t)nthreads - 1) / (uint32_t)nthreads;
+    printf("{\"wrkmem\": \"%s\", \"avoided_cpu\": %d, \"sample_bytes\": %.0f, "
+           "\"per_thread_working_set_bytes\": %.0f, ",
+           zero_wrk ? "zero" : "reuse", avoid, sample_bytes, sample_bytes / nblocks * per_thr);
+    printf("\"kind\": \"%s\", \"threads\": %d, \"affinity_cpus\": %d, \"pin\": \"%s\", \"blocks\": %u, "
            "\"decompress_Bps\": %.1f, \"compress_Bps\": %.1f, \"decompress_s\": %.3f, "
            "\"compress_s\": %.3f, \"byte_identical\": %u, \"decoded\": %u, \"errors\": %d, "
            "\"per_thread_decompress_Bps\": [",

@@ -354,7 +354,32 @@ def manifest(ref: Ref):
     return [(e["name"], e["nblocks"]) for e in entries]
 
 
+def order_entry(ref: Ref):
+    """A batch with more mixed 4-256 KiB ITB blocks than one resident round of
+    the encoder's workgroups (4,096 on 256 CUs), so the device batch takes the
+    largest-first start order (lzo1x_order_kernel) before lzo1x_encode_gdict1
+    (VERDICT r5 item 3).  Added to manifest.json in place: `python
+    tests/golden/make_golden.py order`."""
+    path = os.path.join(OUT, "manifest.json")
+    with open(path) as f:
+        man = json.load(f)
+    e = batch_entry(ref, "C4_order", synth.ITB, 200000, list(synth.mixed_sizes(8192, 8)),
+                    "config C4 beyond one resident round: 8192 mixed 4-256 KiB ITB-like blocks "
+                    "(the start-order path)")
+    man["batches"] = [b for b in man["batches"] if b["name"] != e["name"]] + [e]
+    with open(path, "w") as f:
+        json.dump(man, f, indent=0)
+    return e["name"], e["nblocks"], sum(batch_sizes_of(e))
+
+
+def batch_sizes_of(e):
+    return e["sizes"] if isinstance(e["sizes"], list) else [e["sizes"]] * e["nblocks"]
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "order":
+        print("manifest entry:", order_entry(Ref()))
+        return
     ref = Ref()
     print("edge vectors:", edge_cases(ref))
     print("malformed rc histogram:", malformed_cases(ref))

@@ -78,7 +78,7 @@ def lzo_oracle_free_compress(dev, gu, d):
     return outs[0]
 
 
-@pytest.mark.parametrize("name", ["C1", "C2C3", "C4_sample", "itb_max", "random_300k",
+@pytest.mark.parametrize("name", ["C1", "C2C3", "C4_sample", "C4_order", "itb_max", "random_300k",
                                   "models64k_random", "models64k_itb", "models64k_zeros",
                                   "models64k_alpha4", "models64k_lzlike", "models64k_text"])
 def test_manifest_batches_round_trip(dev, gu, manifest, name):
@@ -97,13 +97,20 @@ def test_manifest_batches_round_trip(dev, gu, manifest, name):
     assert hashlib.sha256(b"".join(outs)).hexdigest() == entry["sha256_input"]
 
 
-@pytest.mark.parametrize("name", ["C1", "C2C3", "C4_sample", "itb_max", "random_300k"])
+@pytest.mark.parametrize("name", ["C1", "C2C3", "C4_sample", "C4_order", "itb_max", "random_300k"])
 def test_manifest_batches_bench_encoder(dev, gu, manifest, name):
     """The same full-size batches through the encoder the bench times (device
     batch with scratch: lzo1x_encode_gdict1_kernel, global dictionaries,
     block tickets on C4's mixed sizes): compressed stream hashes to the
-    reference's."""
+    reference's.  C4_order has more blocks than one
+    resident round, so the batch starts largest first (lzo1x_order_kernel),
+    the C4 regime."""
     entry = next(e for e in manifest if e["name"] == name)
+    if name == "C4_order":
+        import ctypes
+        lib = lzo.load()
+        lib.lzo_mi355x_fast_resident_blocks.restype = ctypes.c_uint32
+        assert entry["nblocks"] > lib.lzo_mi355x_fast_resident_blocks()
     arena, offs, lens = synth.batch(entry["model_id"], entry["seed0"], batch_sizes(entry))
     blocks = [arena[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
               for b in range(len(lens))]

@@ -106,6 +106,17 @@ def test_oracle_manifest_batches(oracle, manifest, name):
     assert hz.hexdigest() == entry["sha256_z"]
 
 
+def test_oracle_manifest_c4_order_sample(oracle, manifest):
+    """C4_order (8,192 mixed blocks, ~1 GiB) is slow on the CPU: the input
+    hash of the whole batch and the first 256 blocks' compressed lengths."""
+    entry = next(e for e in manifest if e["name"] == "C4_order")
+    sizes = batch_sizes(entry)
+    arena, offs, lens = synth.batch(entry["model_id"], entry["seed0"], sizes[:256])
+    for b in range(256):
+        d = arena[int(offs[b]): int(offs[b]) + int(lens[b])].tobytes()
+        assert len(oracle.compress(d)) == entry["zlens"][b]
+
+
 def test_oracle_manifest_c1_sample(oracle, manifest):
     """C1 (1K random 64 KiB) is slow on the CPU; check the first 64 block lengths."""
     entry = next(e for e in manifest if e["name"] == "C1")
