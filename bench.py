@@ -237,12 +237,12 @@ def cpu_baseline(plain, comps, seconds, roundtrip=True):
         "resident_zeroed_wrkmem": {"compress_value": _leg(one_res)["compress_value"],
                                    "decompress_value": _leg(one_res)["decompress_value"],
                                    "working_set_bytes": one_res["per_thread_working_set_bytes"]},
-        "note": ("one_core (and value) reuse each thread's wrkmem across calls without clearing "
-                 "it, as mds/itb.c:2913 does, and cycle the whole sample: the dictionary then "
-                 "holds the previous blocks' pointers, and lzo1x_1_compress runs slower than "
-                 "on a zeroed wrkmem; the single-call figure (other_configs.single ... ref) "
-                 "zeroes the wrkmem and repeats one cache-resident block, the "
-                 "resident_zeroed_wrkmem regime here")}
+        "note": (f"one_core (and value) cycle the whole sample, {runs[1]['per_thread_working_set_bytes'] / 1e6:.1f} MB "
+                 "per thread, beyond one core's caches, and reuse each thread's wrkmem without clearing "
+                 "it, as mds/itb.c:2913 does; the single-call figure (other_configs.single, 'ref') repeats "
+                 "one cache-resident block with the wrkmem zeroed per call: the resident_zeroed_wrkmem "
+                 f"regime, {_leg(one_res)['compress_value']:.2f} against {one['compress_value']:.2f} GiB/s "
+                 "compress here; cycled_zeroed_wrkmem separates the two effects")}
     return {"value": top["value"], "unit": "GiB/s", "cores": share,
             "affinity_cpus": affinity_cpus(), "host": host_cpu_info(),
             "kind": j["kind"], "compress_value": top["compress_value"],
