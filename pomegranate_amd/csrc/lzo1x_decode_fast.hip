@@ -106,6 +106,12 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #ifndef POM_DUTY_EVERY
 #define POM_DUTY_EVERY 4                         // parser pass-1 iterations between writer duties
 #endif
+#ifndef POM_EXEC_STORES
+#define POM_EXEC_STORES 1                        // the executor stores its own output (the parser only parses)
+#endif
+#ifndef POM_STORE_LAG
+#define POM_STORE_LAG 2048                       // executor stores trail its production by this much
+#endif
 constexpr uint32_t kRing = POM_RING;             // recent output kept in LDS
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kMirror = 32;                 // ring[0, 16) mirrored after its end (+ write spill)
@@ -467,6 +473,68 @@ __device__ __forceinline__ Step decode_step(const FastLds& s, const Blk& k, uint
     return r;
 }
 
+// Wave-uniform form of decode_step for the parser's exact walks (the scalar
+// scan below walks one segment's true path with every lane at the same
+// point): the two stage dwords are made scalar with readfirstlane, so the
+// decode runs on the scalar unit -- a few SALU per field instead of a VALU
+// instruction for all 64 lanes (~55 per instruction decoded).  Same fields as
+// decode_step; the rare instructions take decode_one (per lane, all alike).
+#ifndef POM_UWALK
+#define POM_UWALK 1
+#endif
+__device__ __forceinline__ Step decode_step_u(const FastLds& s, const Blk& k, uint32_t pos, uint32_t st)
+{
+    const uint32_t rel = pos - k.P;
+    const bool inwin = rel + 8 <= kStageBytes && pos < k.z;
+    const uint32_t wi = inwin ? rel >> 2 : 0u;
+    const uint32_t w0 = __builtin_amdgcn_readfirstlane(s.stage[wi]);
+    const uint32_t w1 = __builtin_amdgcn_readfirstlane(s.stage[wi + 1]);
+    const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8u * (rel & 3u)));
+    const uint32_t t = lo & 0xFFu, b1 = (lo >> 8) & 0xFFu;
+    const bool flit = st == ST_F && t > 17;                        // :3357-3365
+    const uint32_t se = st == ST_F ? ST_A : st;
+    const bool lit = !flit && se == ST_A && t < 16;                // :3367-3414
+    const bool m1 = !flit && !lit && t < 16;
+    const bool m2 = !flit && t >= 64;
+    const bool m3 = !flit && t >= 32 && t < 64;
+    const bool m4 = !flit && t >= 16 && t < 32;
+    const bool ext = (lit && t == 0) || (m3 && (t & 31) == 0) || (m4 && (t & 7) == 0);
+    const bool needs_slow = !inwin || (ext && b1 == 0);            // 255-chunk extension
+    const uint32_t e = ext ? 1u : 0u;
+    const uint32_t o16 = (lo >> (8u + 8u * e)) & 0xFFFFu;          // bytes 1+e, 2+e
+    const uint32_t dd4 = ((t & 8u) << 11) + (o16 >> 2);
+    const uint32_t used = (m1 || m2) ? 2u : 3u + e;                // match instruction bytes
+    const uint32_t tl = (lo >> (8u * (used - 2u))) & 3u;           // match_done, :3650
+    const uint32_t nlit = flit ? t - 17 : (ext ? 15u + b1 : t) + 3u;
+    const uint32_t L = m1 ? (se == ST_B ? 3u : 2u)
+                     : m2 ? (t >> 5) + 1u
+                     : m3 ? (ext ? 31u + b1 : (t & 31u)) + 2u
+                          : (ext ? 7u + b1 : (t & 7u)) + 2u;
+    const bool eof = m4 && dd4 == 0;                               // :3580
+    const bool islit = flit || lit;
+    const uint32_t hdr = flit ? 1u : 1u + e;                       // literal-run header bytes
+    Step r;
+    r.eof = eof;
+    r.aL = eof ? 0u : islit ? nlit : L;
+    r.aS = 0;                                                      // (the walks count ops only)
+    r.bL = (islit || eof) ? 0u : tl;
+    r.bS = 0;
+    r.pos = islit ? pos + hdr + nlit : pos + used + (eof ? 0u : tl);
+    r.st = islit ? (flit && nlit < 4 ? ST_C : ST_B) : (tl && !eof ? ST_C : ST_A);
+    r.bad = eof ? r.pos != k.z : r.pos > k.z;
+    if (__builtin_expect(needs_slow, 0)) {
+        // (every lane decodes the same instruction: keep the fields scalar)
+        const Step q = decode_one(s, k, pos, st);
+        r.pos = __builtin_amdgcn_readfirstlane(q.pos);
+        r.st = __builtin_amdgcn_readfirstlane(q.st);
+        r.aL = __builtin_amdgcn_readfirstlane(q.aL);
+        r.bL = __builtin_amdgcn_readfirstlane(q.bL);
+        r.eof = __builtin_amdgcn_readfirstlane(q.eof ? 1u : 0u) != 0;
+        r.bad = __builtin_amdgcn_readfirstlane(q.bad ? 1u : 0u) != 0;
+    }
+    return r;
+}
+
 // Output / input byte helpers -------------------------------------------------
 __device__ __forceinline__ uint32_t ring_byte(const FastLds& s, uint32_t y)
 {
@@ -699,7 +767,7 @@ __device__ __forceinline__ WalkRes walk_true(const FastLds& S, const Blk& k, uin
             }
         }
         bool slow = false;
-        const Step r = decode_step<SPEC>(S, k, pos, st, &slow);
+        const Step r = (!SPEC && POM_UWALK) ? decode_step_u(S, k, pos, st) : decode_step<SPEC>(S, k, pos, st, &slow);
         if (SPEC && slow) {
             w.fl = FL_UNK;
             break;
@@ -772,6 +840,8 @@ struct WState {
 
 __device__ __forceinline__ uint32_t writer_duty(FastLds& S, uint8_t* out, uint32_t l, WState& w)
 {
+    if (POM_EXEC_STORES)
+        return 0;                                      // (the executor stores its own output)
     const uint32_t state = lds_load(&S.state);
     const uint32_t prod = lds_load(&S.produced);
     if (state == 2)
@@ -805,6 +875,23 @@ __device__ __forceinline__ uint32_t writer_duty(FastLds& S, uint8_t* out, uint32
     return 0;
 }
 
+// Executor-side stores (POM_EXEC_STORES): the executor stores ring bytes
+// [at, end) of its own output, one dwordx4 per lane for whole 16-byte pieces
+// (bytes past `end` are not written).  Its LDS reads of the ring come before
+// any later ring write of the wave (LDS accesses of a wave complete in order),
+// so a slot may be overwritten by the next step as soon as its store is issued.
+__device__ __forceinline__ void exec_store(const FastLds& S, uint8_t* out, uint32_t l, uint32_t at, uint32_t end)
+{
+    const uint32_t x = at + 16 * l;
+    if (x + 16 <= end) {
+        const uint4 v = *(const uint4*)&S.ring[(x & kRingMask) >> 2];
+        *(uint4*)(out + x) = v;
+    } else if (x < end) {
+        for (uint32_t q = 0; x + q < end; q++)
+            out[x + q] = (uint8_t)ring_byte(S, x + q);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Parser wave: pieces in stream order with exact entries (the true exit of
 // the previous piece), ops to slot q mod kSlots; writer duty in between.
@@ -824,7 +911,8 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
             k.P = entry_pos - (entry_pos % kPiece);
         // a free slot: the executor is done with piece q - kSlots
         for (uint32_t spin = 0; q - lds_load(&S.consumed) >= kSlots; spin++) {
-            if (writer_duty(S, k.out, l, w) == 2 || spin > (1u << 22))
+            if (writer_duty(S, k.out, l, w) == 2 || spin > (1u << 22) ||
+                (POM_EXEC_STORES && lds_load(&S.state) == 2))
                 return;                        // the executor refused (or is stuck)
             __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
         }
@@ -1093,8 +1181,8 @@ __device__ __forceinline__ void parser_wave(FastLds& S, Blk k, uint2* __restrict
             return;
         STAMP(PH_PDUTY);
     }
-    // parse finished: writer only
-    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+    // parse finished: writer only (with executor-side stores: nothing left)
+    for (uint32_t spin = 0; !POM_EXEC_STORES && spin < (1u << 22); spin++) {
         if (writer_duty(S, k.out, l, w) != 0)
             break;
         __builtin_amdgcn_s_sleep(POM_WRITER_SLEEP);
@@ -1436,6 +1524,9 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
     const uint32_t psel1 = psel0 + (uint32_t)sizeof(S.psel[0]);
     uint32_t carry = 0;                        // output produced so far
     uint32_t issued_seen = 0, landed_seen = 0; // last `issued` / `landed` read
+    // (POM_EXEC_STORES) output bytes whose stores this wave issued; landed_seen
+    // is then the stored count at its last vmcnt(0)
+    uint32_t stored = 0;
     uint32_t tag = 0;                          // step counter for the chunk tags
     uint32_t published = 0;                    // last `produced` handed to the writer
     uint32_t q = 0, w0 = 0, total_ops = 0;     // piece, window start, piece's op count
@@ -1497,17 +1588,23 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             }
             // what the source copy does not find in the ring (below carry -
             // kRing) it reads from HBM: that output must have landed
-            if (carry > kRing)
+            if (!POM_EXEC_STORES && carry > kRing)
                 landed_seen = wait_landed(S, carry - kRing, landed_seen, refuse);
             if (refuse) {
                 reason = RS_LANDED;
                 break;
             }
-            // prefetch the next window's op records of this piece
+            // prefetch the next window's op records of this piece (with
+            // executor-side stores: after the landed check below, whose
+            // vmcnt(0) would otherwise wait for it)
             have_pf = w0 + kWave < total_ops;
-            if (have_pf && w0 + kWave + l < total_ops)
-                pf = __hip_atomic_load((const uint64_t*)(slot + w0 + kWave + l), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+            auto prefetch_records = [&]() {
+                if (have_pf && w0 + kWave + l < total_ops)
+                    pf = __hip_atomic_load((const uint64_t*)(slot + w0 + kWave + l), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            };
+            if (!POM_EXEC_STORES)
+                prefetch_records();
             STAMP(PH_WLOAD);
             if (STAMPS)
                 acc[CN_WINDOWS] += 1;
@@ -1534,6 +1631,17 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
             const uint32_t ipos = Sv & ~kLitFlag;
             uint32_t db = lit ? kLitFlag | (kLinHbm + ipos) : o - Sv;
             uint32_t dp = (!lit && Sv < L) ? Sv : 0u;
+            if (POM_EXEC_STORES) {
+                // sources older than the ring are read back from HBM: the
+                // stores of those bytes (issued before their slots were
+                // reused, so stored >= carry - kRing) must have completed
+                if (carry > kRing && landed_seen < carry - kRing &&
+                    wave_ballot(l < nwin && !lit && db < carry - kRing)) {
+                    __builtin_amdgcn_s_waitcnt(0x0F70);                      // vmcnt(0)
+                    landed_seen = stored;
+                }
+                prefetch_records();
+            }
             STAMP(PH_WSCAN);
             const SrcCopy fc = src_issue(S, k, l, nwin, carry, landed_seen, o, L, dp, lit, ipos, db);
             STAMP(PH_FARI);
@@ -1637,8 +1745,19 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     const uint32_t step_end = lane_read(x + len, nl - 1);
                     STAMP(PH_FLAGS);
                     // ring space: the stores of what the slots of [xs, step_end)
-                    // held must have been issued
-                    for (uint32_t spin = 0; step_end > issued_seen + kRing; spin++) {
+                    // held must have been issued.  Executor-side stores: this
+                    // wave issues them itself, whole 1-KiB pieces of final
+                    // output (below xs), trailing its production by
+                    // POM_STORE_LAG so that a read back from HBM rarely waits
+                    // for a store still in flight.
+                    if (POM_EXEC_STORES) {
+                        const uint32_t want = xs > POM_STORE_LAG ? xs - POM_STORE_LAG : 0u;
+                        while (stored + kChunk <= want || stored + kRing < step_end) {
+                            exec_store(S, k.out, l, stored, stored + kChunk);
+                            stored += kChunk;
+                        }
+                    }
+                    for (uint32_t spin = 0; !POM_EXEC_STORES && step_end > issued_seen + kRing; spin++) {
                         if (spin > (1u << 20)) {       // writer stuck: let the exact path redo it
                             refuse = true;
                             reason = RS_SPACE;
@@ -1704,8 +1823,20 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                                      sh);
                     }
                     if (mhbm) {
-                        if ((mhbm & mask_nonneg(op.y)) && xs + 16u > kRing)   // (!lin: bit 31 clear)
-                            landed_seen = wait_landed(S, xs + 16u - kRing, landed_seen, refuse);
+                        if ((mhbm & mask_nonneg(op.y)) && xs + 16u > kRing) {  // (!lin: bit 31 clear)
+                            if (!POM_EXEC_STORES)
+                                landed_seen = wait_landed(S, xs + 16u - kRing, landed_seen, refuse);
+                            else if (landed_seen < xs + 16u - kRing) {
+                                // (stored >= step_end - kRing covers every byte read here:
+                                // sources below xs - kRing, 16 bytes from there)
+                                while (stored < xs + 16u - kRing) {
+                                    exec_store(S, k.out, l, stored, stored + kChunk);
+                                    stored += kChunk;
+                                }
+                                __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+                                landed_seen = stored;
+                            }
+                        }
                         const uint8_t* gb = lin ? k.in - kLinHbm : k.out;
                         if (hA)
                             vA = global_read16(gb + aA, 0u, small ? p : two ? n1 : len);
@@ -1765,7 +1896,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     STAMP(PH_GATHER);
                     // bytes below step_end are final: hand them over once a
                     // 1-KiB store chunk is complete (the writer stores whole chunks)
-                    if (!POM_LAZY_PUB || (step_end ^ published) >= kChunk) {
+                    if (!POM_EXEC_STORES && (!POM_LAZY_PUB || (step_end ^ published) >= kChunk)) {
                         lds_store(&S.produced, step_end);
                         published = step_end;
                     }
@@ -1791,11 +1922,20 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
         for (int i = 0; i < PH_N; i++)
             if (!parser_slot(i))
                 stamps[(size_t)b * kStampSlots + i] = acc[i];
+    if (POM_EXEC_STORES && !refuse) {
+        // the rest of the output, then wait for every store to land
+        for (; stored < carry; stored += kChunk)
+            exec_store(S, k.out, l, stored, carry - stored < kChunk ? carry : stored + kChunk);
+        __builtin_amdgcn_s_waitcnt(0x0F70);                  // vmcnt(0)
+        stored = carry;
+    }
     if (l == 0) {
         if (refuse) {
             lds_store(&S.why, reason);
             lds_store(&S.state, 2u);
         } else {
+            if (POM_EXEC_STORES)
+                lds_store(&S.landed, carry);                 // (block_close checks landed == produced)
             lds_store(&S.produced, carry);
             lds_store(&S.state, 1u);
         }
