@@ -95,7 +95,7 @@ static_assert((kSlots & (kSlots - 1)) == 0, "slots: power of two");
 #define POM_PRIO_STEP 10240                      // executor priority drops every this many bytes left
 #endif
 #ifndef POM_PARSER_PRIO
-#define POM_PARSER_PRIO 3                        // final-round parser wave priority
+#define POM_PARSER_PRIO 1                        // final-round parser wave priority (3 while it was also the writer)
 #endif
 #ifndef POM_LAZY_PUB
 #define POM_LAZY_PUB 1                           // hand output to the writer per completed 1-KiB chunk

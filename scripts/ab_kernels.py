@@ -45,6 +45,7 @@ ol = torch.zeros_like(zl); st = torch.zeros_like(zl)
 dscr = torch.empty(lzo.decompress_scratch_bytes(nb), dtype=torch.uint8, device=dev)
 d = timed(lambda: lzo.decompress_dev(zsrc, ob, ol, st, dscr))
 ok = torch.equal(out, src.arena) and bool((st == 0).all()) and bool((zs == 0).all())
+fb = int(dscr[:4].view(torch.int32).item())              # blocks the fast decoder handed over
 print(f"{os.path.basename(a.lib or lzo.LIB_PATH)}: compress {c[0]:.3f} ms (min {c[1]:.3f}), "
-      f"decompress {d[0]:.3f} ms (min {d[1]:.3f}), z {int(zl.long().sum())}, ok {ok}", flush=True)
+      f"decompress {d[0]:.3f} ms (min {d[1]:.3f}), z {int(zl.long().sum())}, ok {ok}, fallback {fb}", flush=True)
 sys.exit(0 if ok else 1)
