@@ -880,6 +880,13 @@ __device__ __forceinline__ uint32_t writer_duty(FastLds& S, uint8_t* out, uint32
 // (bytes past `end` are not written).  Its LDS reads of the ring come before
 // any later ring write of the wave (LDS accesses of a wave complete in order),
 // so a slot may be overwritten by the next step as soon as its store is issued.
+__device__ __forceinline__ void exec_store_chunk(const FastLds& S, uint8_t* out, uint32_t l, uint32_t at)
+{
+    // (a whole 1-KiB piece: no partial lanes, no branches in the step loop)
+    const uint32_t x = at + 16 * l;
+    const uint4 v = *(const uint4*)&S.ring[(x & kRingMask) >> 2];
+    *(uint4*)(out + x) = v;
+}
 __device__ __forceinline__ void exec_store(const FastLds& S, uint8_t* out, uint32_t l, uint32_t at, uint32_t end)
 {
     const uint32_t x = at + 16 * l;
@@ -1742,7 +1749,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     const uint32_t len = live ? (rem < 16u ? rem : 16u) : 0u;
                     const uint32_t nl = c_end - C < (uint32_t)kWave ? c_end - C : (uint32_t)kWave;
                     const uint32_t xs = lane_read(x, 0);
-                    const uint32_t step_end = lane_read(x + len, nl - 1);
+                    const uint32_t step_end = POM_EXEC_STORES ? 0u : lane_read(x + len, nl - 1);
                     STAMP(PH_FLAGS);
                     // ring space: the stores of what the slots of [xs, step_end)
                     // held must have been issued.  Executor-side stores: this
@@ -1752,8 +1759,9 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     // for a store still in flight.
                     if (POM_EXEC_STORES) {
                         const uint32_t want = xs > POM_STORE_LAG ? xs - POM_STORE_LAG : 0u;
-                        while (stored + kChunk <= want || stored + kRing < step_end) {
-                            exec_store(S, k.out, l, stored, stored + kChunk);
+                        // (xs + kStepSpan bounds step_end without its readlane)
+                        while (stored + kChunk <= want || stored + kRing < (POM_EXEC_STORES ? xs + kStepSpan : step_end)) {
+                            exec_store_chunk(S, k.out, l, stored);
                             stored += kChunk;
                         }
                     }
@@ -1830,7 +1838,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                                 // (stored >= step_end - kRing covers every byte read here:
                                 // sources below xs - kRing, 16 bytes from there)
                                 while (stored < xs + 16u - kRing) {
-                                    exec_store(S, k.out, l, stored, stored + kChunk);
+                                    exec_store_chunk(S, k.out, l, stored);
                                     stored += kChunk;
                                 }
                                 __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
