@@ -674,6 +674,9 @@ typedef __attribute__((address_space(1))) const uint32_t gdword;
 #ifndef POM_FAR_SC1
 #define POM_FAR_SC1 1                            // far reads: agent-scope (L2-allocating) loads instead of non-temporal
 #endif
+#ifndef POM_FAR_UNCOND
+#define POM_FAR_UNCOND 1                         // far reads: all five loads unconditional (clamped addresses)
+#endif
 template <bool NT>
 __device__ __forceinline__ uint32_t global_dword(const uint8_t* p)
 {
@@ -702,6 +705,17 @@ __device__ __forceinline__ uint4 global_read16(const uint8_t* p, uint32_t lo, ui
     gdword* q = (gdword*)(a & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(a & 3);
     uint32_t w[5];
+#if POM_FAR_UNCOND
+    // every load issued (no exec branch per dword): a dword outside
+    // [i0, i1] reads dword i0 or i1 again and is then dropped
+    const uint32_t i0 = (lo + sh) >> 2, i1 = (hi + sh - 1) >> 2;
+#pragma unroll
+    for (uint32_t i = 0; i < 5; i++) {
+        const uint32_t j = i < i0 ? i0 : i > i1 ? i1 : i;
+        const uint32_t v = __hip_atomic_load((uint32_t*)(q + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        w[i] = i == j ? v : 0u;
+    }
+#else
 #pragma unroll
     for (uint32_t i = 0; i < 5; i++) {
         // aligned dword i holds bytes 4i - sh .. 4i + 3 - sh of the span
@@ -709,6 +723,7 @@ __device__ __forceinline__ uint4 global_read16(const uint8_t* p, uint32_t lo, ui
         w[i] = use ? (POM_FAR_SC1 ? __hip_atomic_load((uint32_t*)(q + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                   : __builtin_nontemporal_load(q + i)) : 0u;
     }
+#endif
     uint4 v;
     v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
     v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
