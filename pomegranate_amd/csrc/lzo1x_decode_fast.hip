@@ -674,6 +674,9 @@ typedef __attribute__((address_space(1))) const uint32_t gdword;
 #ifndef POM_FAR_SC1
 #define POM_FAR_SC1 1                            // far reads: agent-scope (L2-allocating) loads instead of non-temporal
 #endif
+#ifndef POM_WRAP_MIRROR
+#define POM_WRAP_MIRROR 1                        // a ring-wrapping chunk: one write through the mirror, then a 16-byte copy
+#endif
 #ifndef POM_FAR_UNCOND
 #define POM_FAR_UNCOND 1                         // far reads: all five loads unconditional (clamped addresses)
 #endif
@@ -1894,6 +1897,19 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                     }
                     // ---- destination: the ring at x -----------------------------
                     const uint32_t xd = x & kRingMask;
+#if POM_WRAP_MIRROR
+                    // a chunk that wraps the ring end runs on into the mirror
+                    // of ring[0, 16); the ring's head is then copied back from
+                    // the mirror (after every lane's mirror write: bytes other
+                    // lanes put in ring[0, 16) this step are in the mirror too)
+                    if (live) {
+                        lds_write_part(base + xd, v, len);
+                        if (xd < 16u)                  // keep the mirror of ring[0, 16)
+                            lds_write_part(base + kRing + xd, v, len);
+                    }
+                    if (mask_lt(kRing, xd + len) && l == 0)     // (len is 0 off the step)
+                        lds_write16(base, lds_read16(base + kRing));
+#else
                     const bool wcross = live && xd + len > kRing;
                     if (live && !wcross) {
                         lds_write_part(base + xd, v, len);
@@ -1915,6 +1931,7 @@ __global__ __launch_bounds__(2 * kWave, POM_WAVES_PER_EU) void lzo1x_decode_fast
                                 }
                         }
                     }
+#endif
                     wave_order();
                     STAMP(PH_GATHER);
                     // bytes below step_end are final: hand them over once a
