@@ -120,6 +120,35 @@ def test_manifest_batches_bench_encoder(dev, gu, manifest, name):
     assert hashlib.sha256(b"".join(comps)).hexdigest() == entry["sha256_z"]
 
 
+def test_bench_encoder_dirty_scratch_reused_dictionaries(dev, gu, oracle):
+    """The bench encoder's dictionaries need no zeroing (round 6: a per-block
+    LDS bitmap of written slots, POM_ENC_OCC).  Twice as many blocks as
+    resident workgroups, so each workgroup codes a second block in the region
+    its first one filled, and every block is a copy of one of two contents:
+    a stale entry of the earlier block would point at equal bytes and turn
+    literals into matches the reference (a zero-filled wrkmem,
+    lib/minilzo.c:2878-2883, 3167-3173) never finds.  The scratch starts
+    filled with 0x5A, not zeros."""
+    lib = lzo.load()
+    lib.lzo_mi355x_fast_resident_blocks.restype = ctypes.c_uint32
+    n = 2 * int(lib.lzo_mi355x_fast_resident_blocks())
+    a = synth.block(synth.ITB, 4242, 8192)
+    b = synth.block(synth.ALPHA4, 4243, 8192)
+    blocks = [a if i % 2 == 0 else b for i in range(n)]
+    src = gu.device_batch(torch, blocks, dev)
+    dst = gu.empty_batch(torch, [lzo.worst_compress(len(x)) for x in blocks], dev, fill=0xA5)
+    olen = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = torch.full((n,), 99, dtype=torch.int32, device=dev)
+    scr = torch.full((lzo.compress_scratch_bytes(n),), 0x5A, dtype=torch.uint8, device=dev)
+    lzo.compress_dev(src, dst, olen, st, scratch=scr)
+    torch.cuda.synchronize()
+    comps = gu.fetch(dst, olen)
+    assert st.cpu().numpy().tolist() == [0] * n
+    want = [oracle.compress(a), oracle.compress(b)]
+    bad = [i for i in range(n) if comps[i] != want[i % 2]]
+    assert not bad, f"{len(bad)} of {n} blocks differ, first {bad[:8]}"
+
+
 def test_long_extensions_past_32_bits(dev, longext):
     """Length extensions of 16,843,008-16,843,010 zero bytes (255 per zero
     passes 2^32 from 16,843,009 on): lzo1x_decompress_safe and a host batch
