@@ -1096,12 +1096,13 @@ __global__ __launch_bounds__(2 * kWave, POM_ENC_RESIDENT / 2) void lzo1x_encode_
 #endif
 static_assert(sizeof(EncLdsT<true>) * POM_ENC_RESIDENT1 <= 160 * 1024, "LDS budget");
 
-__global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdict1_kernel(
+template <bool STAMPS>
+__device__ __forceinline__ void gdict1_body(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
     const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
-    uint8_t* __restrict__ dicts, const uint32_t* __restrict__ order)
+    uint8_t* __restrict__ dicts, const uint32_t* __restrict__ order, uint64_t* __restrict__ stamps)
 {
     __shared__ EncLdsT<true> S;
     Dict<true> D;
@@ -1125,10 +1126,36 @@ __global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdi
         E.ost = status;
         E.blk = b;
         E.prio = !dyn;                               // (block tickets: mixed sizes, no priority)
-        uint64_t acc[EP_N];
-        parse_wave<false, true, true>(S, D, in, n, l, acc, &E);
+        uint64_t acc[EP_N] = {};
+        parse_wave<STAMPS, true, true>(S, D, in, n, l, acc, &E);
+        if (STAMPS && l == 0)
+            for (int i = 0; i < EP_N; i++)
+                stamps[(size_t)b * kEncStampSlots + i] = acc[i];
         wave_order();
     }
+}
+
+__global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdict1_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
+    uint8_t* __restrict__ dicts, const uint32_t* __restrict__ order)
+{
+    gdict1_body<false>(src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks, dicts,
+                       order, nullptr);
+}
+
+// (diagnostic) the same with the parse wave's phase stamps
+__global__ __launch_bounds__(kWave, POM_ENC_RESIDENT1 / 4) void lzo1x_encode_gdict1_stamps_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ status, uint32_t nblocks,
+    uint8_t* __restrict__ dicts, uint64_t* __restrict__ stamps)
+{
+    gdict1_body<true>(src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks, dicts,
+                      nullptr, stamps);
 }
 
 }  // namespace
@@ -1248,6 +1275,25 @@ extern "C" int lzo_mi355x_debug_compress_gdict_stamps(const uint8_t* src, const 
     if (grid == 0 || (grid < nblocks && hipMemsetAsync(scratch, 0, sizeof(uint32_t), stream) != hipSuccess))
         return -1;
     hipLaunchKernelGGL(lzo1x_encode_gdict_kernel<true>, dim3(grid), dim3(2 * kWave), 0, stream,
+                       src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
+                       (uint8_t*)scratch, stamps);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Diagnostic: the one-wave global-dictionary encoder (the bench's) with
+// parse-wave phase stamps (16 x u64 per block; no start order).
+extern "C" int lzo_mi355x_debug_compress_gdict1_stamps(const uint8_t* src, const uint64_t* src_off,
+                                                       const uint32_t* src_len, uint8_t* dst,
+                                                       const uint64_t* dst_off,
+                                                       const uint32_t* dst_cap, uint32_t* out_len,
+                                                       int32_t* status, uint32_t nblocks,
+                                                       void* scratch, size_t scratch_bytes,
+                                                       uint64_t* stamps, hipStream_t stream)
+{
+    const uint32_t grid = enc_grid(scratch_bytes, nblocks);
+    if (grid == 0 || (grid < nblocks && hipMemsetAsync(scratch, 0, sizeof(uint32_t), stream) != hipSuccess))
+        return -1;
+    hipLaunchKernelGGL(lzo1x_encode_gdict1_stamps_kernel, dim3(grid), dim3(kWave), 0, stream,
                        src, src_off, src_len, dst, dst_off, dst_cap, out_len, status, nblocks,
                        (uint8_t*)scratch, stamps);
     return hipGetLastError() == hipSuccess ? 0 : -1;

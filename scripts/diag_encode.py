@@ -39,16 +39,22 @@ if gfn is not None:
     gfn.restype = ctypes.c_int
     gfn.argtypes = [ctypes.c_void_p] * 8 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
                                             ctypes.c_void_p, ctypes.c_void_p]
+g1fn = getattr(lib, "lzo_mi355x_debug_compress_gdict1_stamps", None)
+if g1fn is not None:
+    g1fn.restype = ctypes.c_int
+    g1fn.argtypes = gfn.argtypes
 p = lambda x: x.data_ptr()
 sh = torch.cuda.current_stream().cuda_stream
 scr = torch.empty(max(lzo.compress_scratch_bytes(nb), 1), dtype=torch.uint8, device=dev)
 ref_out = None
 gstamps = torch.zeros(nb * SLOTS, dtype=torch.int64, device=dev)
-for mode in ("lds", "gdict", "stamps", "gstamps"):
-    if mode in ("stamps", "gstamps") and (fn is None or gfn is None or a.nostamps):
+g1stamps = torch.zeros(nb * SLOTS, dtype=torch.int64, device=dev)
+STAMPED = ("stamps", "gstamps", "g1stamps")
+for mode in ("lds", "gdict", "stamps", "gstamps", "g1stamps"):
+    if mode in STAMPED and (fn is None or gfn is None or g1fn is None or a.nostamps):
         continue
     ts = []
-    for _ in range(1 if mode in ("stamps", "gstamps") else 5):
+    for _ in range(1 if mode in STAMPED else 5):
         za.zero_()
         e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -57,12 +63,15 @@ for mode in ("lds", "gdict", "stamps", "gstamps"):
         elif mode == "gstamps":
             gfn(p(src.arena), p(src.off), p(src.length), p(za), p(zb.off), p(zb.length), p(zl), p(zs), nb,
                 p(scr), scr.numel(), p(gstamps), sh)
+        elif mode == "g1stamps":               # (the bench's one-wave kernel)
+            g1fn(p(src.arena), p(src.off), p(src.length), p(za), p(zb.off), p(zb.length), p(zl), p(zs), nb,
+                 p(scr), scr.numel(), p(g1stamps), sh)
         else:
             lzo.compress_dev(src, zb, zl, zs, scratch=scr if mode == "gdict" else None)
         e1.record(); torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     same = ""
-    if mode not in ("stamps", "gstamps"):
+    if mode not in STAMPED:
         got = (za.clone(), zl.clone())
         if ref_out is None:
             ref_out = got
@@ -73,7 +82,7 @@ if fn is None or a.nostamps:
     sys.exit(0)
 phases = ["setup", "probe", "cand", "path", "claim", "tok", "dict", "pushwait"]
 counts = ["windows", "extend", "tokens", "pathit", "extit", "end_cross", "end_cap", "fwd"]
-for name, t_ in (("lds", stamps), ("gdict", gstamps)):
+for name, t_ in (("lds", stamps), ("gdict", gstamps), ("gdict1", g1stamps)):
     st = t_.view(nb, SLOTS).double().cpu().numpy()
     print(name, "parse cycles/block (mean):", {n: int(st[:, i].mean()) for i, n in enumerate(phases)},
           "total", int(st[:, :len(phases)].sum(1).mean()))
